@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Run in the build container (needs /root/reference and `make -C oracle ref`):
+
+    python tests/golden/gen_golden.py
+
+The expected outputs are produced by oracle/_ref/libqiref.so, i.e. QuadIron's
+own RsFnt<uint32_t> (FecCode::encode_blocks_vertical / decode_blocks_vertical,
+src/fec_base.h:1066-1321) and Properties::fnt_serialize/deserialize
+(src/property.h:104-142) compiled from the reference sources.  The only input
+the plain-C oracle contributes is the *crafting* of OOR-forcing data columns
+(choose d0 so that a chosen output equals 65536); the expected values for
+those columns still come from the reference.
+
+Fixtures are .npz files holding only integer arrays (load with
+numpy.load(allow_pickle=False)).
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.path.join(ROOT, "oracle", "_ref", "libqiref.so")
+ORA = os.path.join(ROOT, "oracle", "liboracle.so")
+Q = 65537
+
+
+class Codec(C.Structure):
+    _fields_ = [(n, C.c_int) for n in
+                ["sys", "k", "m", "code_len", "n_outputs", "n", "data_len",
+                 "len_2k"]] + [("r", C.c_uint32)]
+
+
+def ptrs(arrs):
+    p = (C.POINTER(C.c_uint8) * len(arrs))()
+    for i, a in enumerate(arrs):
+        p[i] = a.ctypes.data_as(C.POINTER(C.c_uint8)) if a is not None else None
+    return p
+
+
+def vp(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def craft_oor(ora, codec, data, rng, n_cols):
+    """Overwrite data[0] at n_cols random columns so that one chosen output
+    row equals 65536 there (exercises the OOR side channel)."""
+    k, no = codec.k, codec.n_outputs
+    words = data.shape[1] // 2
+    first = k if codec.sys else 0
+    cw = (C.c_uint32 * codec.n)()
+    din = (C.c_uint32 * k)()
+    ids = (C.c_uint32 * k)(*range(k))
+    ctx = C.create_string_buffer(8 * 1024 * 4 + 64)
+    if codec.sys:
+        ora.qo_ctx_init(C.byref(codec), ctx, ids)
+
+    def enc(vals):
+        for t in range(k):
+            din[t] = int(vals[t])
+        ora.qo_encode_column(C.byref(codec), ctx if codec.sys else None,
+                             din, cw)
+        return [cw[first + i] for i in range(no)]
+
+    e0 = [1] + [0] * (k - 1)
+    a = enc(e0)
+    done = 0
+    for j in rng.permutation(words):
+        if done >= n_cols:
+            break
+        col = data[:, 2 * j].astype(np.uint32) | (
+            data[:, 2 * j + 1].astype(np.uint32) << 8)
+        col[0] = 0
+        b = enc(col)
+        i = int(rng.integers(0, no))
+        if a[i] == 0:
+            continue
+        d0 = ((65536 - b[i]) % Q) * pow(a[i], Q - 2, Q) % Q
+        if d0 == 65536:
+            continue
+        data[0, 2 * j] = d0 & 0xFF
+        data[0, 2 * j + 1] = d0 >> 8
+        done += 1
+
+
+def gen_blocks(ref, ora, name, k, m, sys_, pkt, block_bytes, seed,
+               n_patterns, n_craft, out_dir):
+    rng = np.random.default_rng(seed)
+    codec = Codec()
+    assert ora.qo_codec_init(C.byref(codec), k, m, sys_) == 0
+    no = codec.n_outputs
+    data = rng.integers(0, 256, (k, block_bytes), dtype=np.uint8)
+    if n_craft:
+        craft_oor(ora, codec, data, rng, n_craft)
+    cap = 64 + block_bytes // 2048
+    outs = np.zeros((no, block_bytes), np.uint8)
+    oor = np.zeros((no, cap), np.uint32)
+    cnt = np.zeros(no, np.uint32)
+    rows = [data[i].copy() for i in range(k)]
+    orow = [outs[i] for i in range(no)]
+    ref.ref_encode_blocks(sys_, k, m, C.c_size_t(pkt), ptrs(rows), ptrs(orow),
+                          C.c_size_t(block_bytes), vp(oor), vp(cnt),
+                          C.c_uint32(cap))
+    assert (cnt <= cap).all()
+    missing = np.zeros((n_patterns, k + m), np.int32)
+    decoded = np.zeros((n_patterns, k, block_bytes), np.uint8)
+    for p in range(n_patterns):
+        miss = rng.choice(k + m, m, replace=False)
+        missing[p, miss] = 1
+        dec = [np.zeros(block_bytes, np.uint8) if (not sys_ or missing[p, i])
+               else data[i].copy() for i in range(k)]
+        par = [None if missing[p, (k + i) if sys_ else i] else outs[i].copy()
+               for i in range(no)]
+        wanted = np.ones(k, np.int32)
+        ok = ref.ref_decode_blocks(sys_, k, m, C.c_size_t(pkt), ptrs(dec),
+                                   ptrs(par), vp(oor), vp(cnt),
+                                   C.c_uint32(cap), vp(missing[p]),
+                                   vp(wanted), C.c_size_t(block_bytes))
+        assert ok == 1
+        decoded[p] = np.stack(dec)
+    np.savez_compressed(
+        os.path.join(out_dir, name + ".npz"),
+        params=np.array([k, m, sys_, pkt, block_bytes, cap], np.int64),
+        data=data, outputs=outs, oor=oor, oor_count=cnt, missing=missing,
+        decoded=decoded)
+    print(f"{name}: k={k} m={m} sys={sys_} block={block_bytes} "
+          f"oor={int(cnt.sum())}")
+
+
+def gen_cabi(ref, ora, name, k, m, sys_, block_bytes, seed, n_patterns,
+             n_craft, out_dir):
+    """C-ABI fixtures: full fragment buffers (FNT1 header + payload)."""
+    rng = np.random.default_rng(seed)
+    codec = Codec()
+    assert ora.qo_codec_init(C.byref(codec), k, m, sys_) == 0
+    md = ref.ref_metadata_size(C.c_size_t(block_bytes))
+    payload = rng.integers(0, 256, (k, block_bytes), dtype=np.uint8)
+    if n_craft:
+        craft_oor(ora, codec, payload, rng, n_craft)
+    data = np.zeros((k, md + block_bytes), np.uint8)
+    data[:, md:] = payload
+    par = np.zeros((m, md + block_bytes), np.uint8)
+    no = codec.n_outputs
+    wanted = np.ones(no, np.int32)
+    d = [data[i].copy() for i in range(k)]
+    p = [par[i].copy() for i in range(m)]
+    rc = ref.ref_c_encode(sys_, k, m, ptrs(d), ptrs(p), vp(wanted),
+                          C.c_size_t(block_bytes))
+    assert rc == 0
+    enc_data, enc_par = np.stack(d), np.stack(p)
+    missing = np.zeros((n_patterns, k + m), np.int32)
+    dec = np.zeros((n_patterns, k, md + block_bytes), np.uint8)
+    dest = np.zeros(n_patterns, np.int32)
+    rec = np.zeros((n_patterns, md + block_bytes), np.uint8)
+    for t in range(n_patterns):
+        miss = rng.choice(k + m, m, replace=False)
+        missing[t, miss] = 1
+        D = [enc_data[i].copy() if not missing[t, i]
+             else np.zeros(md + block_bytes, np.uint8) for i in range(k)]
+        P = [enc_par[i].copy() if not missing[t, k + i]
+             else np.zeros(md + block_bytes, np.uint8) for i in range(m)]
+        assert ref.ref_c_decode(sys_, k, m, ptrs(D), ptrs(P),
+                                vp(missing[t]), C.c_size_t(block_bytes)) == 0
+        dec[t] = np.stack(D)
+        dest[t] = int(rng.choice(miss))
+        D = [enc_data[i].copy() if not missing[t, i]
+             else np.zeros(md + block_bytes, np.uint8) for i in range(k)]
+        P = [enc_par[i].copy() if not missing[t, k + i]
+             else np.zeros(md + block_bytes, np.uint8) for i in range(m)]
+        assert ref.ref_c_reconstruct(sys_, k, m, ptrs(D), ptrs(P),
+                                     vp(missing[t]), C.c_uint(dest[t]),
+                                     C.c_size_t(block_bytes)) == 0
+        rec[t] = (D + P)[dest[t]]
+    np.savez_compressed(
+        os.path.join(out_dir, name + ".npz"),
+        params=np.array([k, m, sys_, block_bytes, md], np.int64),
+        data=data, enc_data=enc_data, enc_parity=enc_par, missing=missing,
+        decoded=dec, dest=dest, reconstructed=rec)
+    print(f"{name}: C-ABI k={k} m={m} sys={sys_} block={block_bytes} md={md}")
+
+
+def main():
+    if not os.path.exists(REF):
+        sys.exit("build the reference first: make -C oracle ref")
+    ref = C.CDLL(REF)
+    ora = C.CDLL(ORA)
+    ora.qo_nth_root.restype = C.c_uint32
+    out = HERE
+    # block-level (vertical) fixtures; pkt sizes differ on purpose (outputs
+    # are pkt-size invariant)
+    gen_blocks(ref, ora, "blk_k4_m4", 4, 4, 0, 512, 4096 + 6, 11, 6, 8, out)
+    gen_blocks(ref, ora, "blk_k16_m48", 16, 48, 0, 1024, 8192 + 2, 12, 6, 24,
+               out)
+    gen_blocks(ref, ora, "blk_k16_m48_sys", 16, 48, 1, 1024, 8192, 13, 6, 24,
+               out)
+    gen_blocks(ref, ora, "blk_k64_m960", 64, 960, 0, 2048, 512, 14, 3, 12, out)
+    gen_blocks(ref, ora, "blk_k3_m3_sys", 3, 3, 1, 8, 2000, 15, 6, 6, out)
+    gen_blocks(ref, ora, "blk_k9_m5", 9, 5, 0, 8, 2001, 16, 6, 6, out)
+    gen_blocks(ref, ora, "blk_k10_m6_sys", 10, 6, 1, 1024, 4096, 17, 6, 8, out)
+    # C-ABI fixtures (pkt_size 1024 inside, headers in front)
+    gen_cabi(ref, ora, "cabi_k3_m3", 3, 3, 0, 10000, 21, 6, 4, out)
+    gen_cabi(ref, ora, "cabi_k3_m3_sys", 3, 3, 1, 10000, 22, 6, 4, out)
+    gen_cabi(ref, ora, "cabi_k16_m48", 16, 48, 0, 4096 + 2, 23, 3, 24, out)
+    gen_cabi(ref, ora, "cabi_k4_m4_big", 4, 4, 0, 2 * 65536 + 10, 25, 2, 12,
+             out)
+    gen_cabi(ref, ora, "cabi_k8_m4_sys", 8, 4, 1, 3 * 4096 + 2, 24, 6, 8, out)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,99 @@
+"""Shared test helpers: ctypes access to the CPU oracle (test infrastructure)
+and golden-fixture loading.  Product code never imports this module."""
+import ctypes as C
+import glob
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+Q = 65537
+
+
+class Codec(C.Structure):
+    _fields_ = [(n, C.c_int) for n in
+                ["sys", "k", "m", "code_len", "n_outputs", "n", "data_len",
+                 "len_2k"]] + [("r", C.c_uint32)]
+
+
+_oracle = None
+
+
+def oracle():
+    """Load (building if needed) the plain-C oracle."""
+    global _oracle
+    if _oracle is None:
+        src = os.path.join(ROOT, "oracle", "qi_oracle.c")
+        if (not os.path.exists(ORACLE_SO)
+                or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src)):
+            subprocess.check_call(["make", "-s", "-C",
+                                   os.path.join(ROOT, "oracle")])
+        lib = C.CDLL(ORACLE_SO)
+        for fn in ("qo_add", "qo_sub", "qo_mul", "qo_exp", "qo_inv",
+                   "qo_nth_root", "qo_code_len"):
+            getattr(lib, fn).restype = C.c_uint32
+        _oracle = lib
+    return _oracle
+
+
+def ptrs(arrs):
+    p = (C.POINTER(C.c_uint8) * len(arrs))()
+    for i, a in enumerate(arrs):
+        p[i] = (a.ctypes.data_as(C.POINTER(C.c_uint8))
+                if a is not None else None)
+    return p
+
+
+def vp(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def codec(k, m, sys_):
+    c = Codec()
+    assert oracle().qo_codec_init(C.byref(c), k, m, int(sys_)) == 0
+    return c
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz"),
+                        allow_pickle=False))
+
+
+def golden_names(prefix):
+    return sorted(os.path.basename(p)[:-4]
+                  for p in glob.glob(os.path.join(GOLDEN, prefix + "*.npz")))
+
+
+def oracle_encode_blocks(k, m, sys_, data, cap=None):
+    """data: (k, B) uint8 -> outputs (n_outputs, B), oor (n_out, cap), cnt."""
+    c = codec(k, m, sys_)
+    B = data.shape[1]
+    cap = cap or (64 + B // 2048)
+    outs = np.zeros((c.n_outputs, B), np.uint8)
+    oor = np.zeros((c.n_outputs, cap), np.uint32)
+    cnt = np.zeros(c.n_outputs, np.uint32)
+    rows = [np.ascontiguousarray(data[i]) for i in range(k)]
+    oracle().qo_encode_blocks(C.byref(c), ptrs(rows),
+                              ptrs([outs[i] for i in range(c.n_outputs)]),
+                              C.c_size_t(B), vp(oor), vp(cnt),
+                              C.c_uint32(cap))
+    return outs, oor, cnt
+
+
+def oracle_decode_blocks(k, m, sys_, outputs, oor, cnt, missing, data=None):
+    """Decode from the encoded outputs with `missing` (code_len flags)."""
+    c = codec(k, m, sys_)
+    B = outputs.shape[1]
+    dec = [np.zeros(B, np.uint8) if (not sys_ or missing[i] or data is None)
+           else data[i].copy() for i in range(k)]
+    par = [None if missing[(k + i) if sys_ else i] else outputs[i].copy()
+           for i in range(c.n_outputs)]
+    missing = np.ascontiguousarray(missing, np.int32)
+    wanted = np.ones(k, np.int32)
+    ok = oracle().qo_decode_blocks(C.byref(c), ptrs(dec), ptrs(par), vp(oor),
+                                   vp(cnt), C.c_uint32(oor.shape[1]),
+                                   vp(missing), vp(wanted), C.c_size_t(B))
+    return ok, np.stack(dec)
