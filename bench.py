@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident RS-FNT encode+decode GB/s per GPU
+(BASELINE.json metric; configs[1]: k=16, n=64, pkt=64 KiB, batch 4096 stripes).
+
+One *step* = encode the whole stripe batch (k=16 data rows -> n=64 coded rows,
+OOR side channel recorded) + build the per-stripe decode contexts (a random
+n-k erasure pattern per stripe) + decode every stripe back to its k data rows.
+Inputs are resident in HBM before the timed region starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--stripes S]
+
+For N > 1 launch one process per GPU (torch.distributed.run); stripes shard
+across ranks with no data-path collective (weak scaling: S stripes per GPU).
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import quadiron_amd as qa  # noqa: E402
+
+K_DATA, M_PAR, PKT_BYTES = 16, 48, 65536
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
+
+
+def alg_bytes(k, m, P):
+    """Algorithmic HBM bytes per stripe:
+    encode (k + n) * 2P, decode (k + k) * 2P."""
+    n = 1
+    while n < k + m:
+        n *= 2
+    return (k + n) * 2 * P, 2 * k * 2 * P
+
+
+def cpu_baseline(k, m, P, threads, stripes_per_thread):
+    """QuadIron's own AVX2 path (oracle/_ref/libqiref_avx2.so, compiled from
+    the reference sources) timed on this host: `threads` independent replicas
+    (the reference bench's -g model) each encoding + decoding
+    `stripes_per_thread` stripes of k x 64 KiB, one fixed n-k erasure
+    pattern.  Falls back to the plain-C oracle port when the reference build
+    is absent."""
+    import ctypes as C
+    ref = os.path.join(ROOT, "oracle", "_ref", "libqiref_avx2.so")
+    enc_b, dec_b = alg_bytes(k, m, P)
+    if os.path.exists(ref):
+        lib = C.CDLL(ref)
+        lib.ref_bench.restype = C.c_double
+        rng = np.random.default_rng(1)
+        missing = np.zeros(k + m, np.int32)
+        missing[rng.choice(k + m, m, replace=False)] = 1
+        e = C.c_double()
+        d = C.c_double()
+        wall = lib.ref_bench(0, k, m, C.c_size_t(P), stripes_per_thread,
+                             threads, missing.ctypes.data_as(C.c_void_p),
+                             C.byref(e), C.byref(d))
+        total = threads * stripes_per_thread * (enc_b + dec_b)
+        return {"value": total / wall / 1e9, "unit": "GB/s", "cores": threads,
+                "kind": "reference",
+                "sample": f"{threads} threads x {stripes_per_thread} stripes "
+                          f"of RS-FNT k={k} n=64 pkt=64KiB enc+dec "
+                          f"(QuadIron AVX2 build, pkt_size {P} words), "
+                          f"wall {wall:.2f}s"}
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--stripes", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-stripes", type=int, default=200)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    k, m, S = K_DATA, M_PAR, args.stripes
+    P = PKT_BYTES // 2
+    plan = qa.Plan(k, m, False)
+    n_out = plan.n_outputs
+    cap = 64
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x51D00001 + rank)
+    data = torch.randint(-32768, 32768, (S, k, P), dtype=torch.int16,
+                         device=dev, generator=g)
+    coded = torch.empty((S, n_out, P), dtype=torch.int16, device=dev)
+    dec = torch.empty((S, k, P), dtype=torch.int16, device=dev)
+    counts = torch.zeros(S * n_out, dtype=torch.int32, device=dev)
+    entries = torch.zeros(S * n_out * cap, dtype=torch.int32, device=dev)
+    # per-stripe erasure pattern: keep a random k-subset of the n ids
+    perm = torch.rand((S, k + m), device=dev, generator=g).argsort(dim=1)
+    ids = perm[:, :k].sort(dim=1).values.to(torch.int16).contiguous()
+    ctx = torch.empty(plan.ctx_bytes(S), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    ev = []
+
+    def step(timed):
+        counts.zero_()
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e2 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        plan.encode(data, coded, counts, entries, cap, stream=stream)
+        if timed:
+            e1.record()
+        plan.decode_ctx(ids, ctx, stream=stream)
+        plan.decode(ctx, ids, coded, dec, counts=counts, entries=entries,
+                    cap=cap, stream=stream)
+        if timed:
+            e2.record()
+            ev.append((e0, e1, e2))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    # correctness of the measured pipeline (outside the timed region)
+    ok = bool(torch.equal(dec, data))
+    oor_max = int(counts.max().item())
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+
+    enc_b, dec_b = alg_bytes(k, m, P)
+    total_bytes = world * S * args.steps * (enc_b + dec_b)
+    value = total_bytes / elapsed / 1e9
+    enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    enc_gbs = S * enc_b / (enc_ms * 1e-3) / 1e9
+    dec_gbs = S * dec_b / (dec_ms * 1e-3) / 1e9
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                traffic = json.load(f).get("encode_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "device-resident encode+decode GB/s per GPU, RS-FNT k=16 "
+                  "n=64 pkt=64KiB",
+        "value": value,
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic",
+        "config": {
+            "workload": "RS-FNT k=16 n=64 pkt=64KiB encode+decode, "
+                        f"batch={S} stripes per GPU",
+            "k": k, "m": m, "n": plan.n, "pkt_bytes": PKT_BYTES,
+            "stripes_per_gpu": S,
+            "decode": "per-stripe random n-k erasures, contexts built "
+                      "on-GPU inside the timed step",
+            "parallelism": f"stripe-sharded x{world} (no collective)",
+        },
+        "per_gpu_value": value / world,
+        "hbm_fraction": value / world / HBM_PEAK_GBS,
+        "encode_kernel_ms": enc_ms,
+        "encode_GBps": enc_gbs,
+        "decode_ms": dec_ms,
+        "decode_GBps": dec_gbs,
+        "roundtrip_ok": ok,
+        "oor_max_per_bucket": oor_max,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "encode_fnt_kernel<16,*>",
+            "achieved": enc_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": enc_gbs / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "bytes_per_launch": S * enc_b,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(k, m, P, threads, args.cpu_stripes)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

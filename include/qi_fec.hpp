@@ -1,0 +1,127 @@
+// qi_fec.hpp -- C++ FecCode-style API of the MI355X RS-FNT engine.
+//
+// Mirrors the part of QuadIron's C++ surface that the C-ABI, the benchmark and
+// ec_driver use (src/fec_base.h:93-294, src/fec_rs_fnt.h:51-270,
+// src/property.h:61-198): RsFnt<uint32_t>(type, word_size, k, m, pkt_size)
+// with the vertical block and stream APIs and the OOR Properties side channel.
+// Every transform runs on the GPU through include/qi_gpu.h; there is no CPU
+// compute path.  word_size 2 (GF(65537)) only.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <istream>
+#include <ostream>
+#include <utility>
+#include <vector>
+
+struct qi_plan;
+
+namespace qi {
+
+static constexpr unsigned OOR_MARK = 1;  // src/property.h:49
+
+// Sparse (location, marker) list of out-of-range symbols of one fragment.
+class Properties {
+  public:
+    enum { FNT1 = 0x464E5431 };
+    void add(size_t location, uint32_t marker)
+    {
+        props.emplace_back(location, marker);
+    }
+    void clear() { props.clear(); }
+    void sort();
+    const std::vector<std::pair<size_t, uint32_t>>& get_map() const
+    {
+        return props;
+    }
+    // FNT1 header (src/property.h:104-142): 0 on success, -1 on error
+    int fnt_serialize(uint32_t* dwords, unsigned n_dwords) const;
+    int fnt_deserialize(const uint32_t* dwords, unsigned n_dwords);
+
+    friend std::istream& operator>>(std::istream& is, Properties& p);
+    friend std::ostream& operator<<(std::ostream& os, const Properties& p);
+
+  private:
+    std::vector<std::pair<size_t, uint32_t>> props;
+};
+
+namespace fec {
+
+enum class FecType { SYSTEMATIC, NON_SYSTEMATIC };
+
+class RsFnt {
+  public:
+    // throws std::invalid_argument (bad parameters / word_size != 2) or
+    // std::runtime_error (no HIP device)
+    RsFnt(FecType type, unsigned word_size, unsigned n_data,
+          unsigned n_parities, size_t pkt_size = 8);
+    ~RsFnt();
+    RsFnt(const RsFnt&) = delete;
+    RsFnt& operator=(const RsFnt&) = delete;
+
+    FecType type;
+    unsigned word_size, n_data, n_parities, code_len, n_outputs;
+    size_t pkt_size, buf_size;
+    unsigned n;
+
+    uint64_t n_encode_ops = 0, n_decode_ops = 0;
+    uint64_t total_enc_usec = 0, total_dec_usec = 0;
+
+    int get_n_outputs() const;  // n (non-systematic) or m (systematic)
+
+    void encode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
+                                std::vector<uint8_t*>& parities_bufs,
+                                std::vector<Properties>& parities_props,
+                                std::vector<bool>& wanted_idxs,
+                                size_t block_size_bytes);
+
+    bool decode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
+                                std::vector<uint8_t*>& parities_bufs,
+                                std::vector<Properties>& parities_props,
+                                std::vector<int>& missing_idxs,
+                                std::vector<bool>& wanted_idxs,
+                                size_t block_size_bytes);
+
+    void encode_streams_vertical(
+        const std::vector<std::istream*>& input_data_bufs,
+        std::vector<std::ostream*>& output_parities_bufs,
+        std::vector<Properties>& output_parities_props);
+
+    bool decode_streams_vertical(
+        const std::vector<std::istream*>& input_data_bufs,
+        const std::vector<std::istream*>& input_parities_bufs,
+        std::vector<Properties>& input_parities_props,
+        std::vector<std::ostream*>& output_data_bufs);
+
+    void reset_stats_enc()
+    {
+        n_encode_ops = 0;
+        total_enc_usec = 0;
+    }
+    void reset_stats_dec()
+    {
+        n_decode_ops = 0;
+        total_dec_usec = 0;
+    }
+
+    qi_plan* plan() const { return plan_; }
+
+  private:
+    // device encode of `words` columns; outputs[i] NULL = not wanted
+    void encode_columns(const uint8_t* const* data, uint8_t* const* outputs,
+                        size_t words, std::vector<Properties>& props,
+                        size_t offset);
+    // device decode of `words` columns from the k selected fragments
+    void decode_columns(const std::vector<int>& ids,
+                        const std::vector<const uint8_t*>& rows,
+                        const std::vector<const Properties*>& props,
+                        uint8_t* const* outputs, size_t words, size_t offset);
+    bool select_fragments(const std::vector<int>& present,
+                          std::vector<int>& ids) const;
+
+    qi_plan* plan_ = nullptr;
+};
+
+}  // namespace fec
+}  // namespace qi

@@ -1,0 +1,118 @@
+/*
+ * qi_gpu.h -- device-level C-ABI of the MI355X RS-FNT engine.
+ *
+ * This is the "thin C-ABI shim" below the drop-in quadiron_c.h boundary: plain
+ * pointers and sizes, no C++ or torch types.  Device pointers are HIP device
+ * memory; `stream` is a hipStream_t passed as void* (NULL = default stream).
+ * All calls are asynchronous on `stream` unless stated.  Errors are negative
+ * ints.
+ *
+ * Semantics follow QuadIron's RsFnt<uint32_t> with word_size 2
+ * (src/fec_rs_fnt.h:51-270): GF(65537), n = ceil2(k+m), root r = 3^(65536/n).
+ *   - NON-SYSTEMATIC encode: outputs 0..k+m-1 = evaluations of the data
+ *     polynomial at r^i (the zero-padded n-point NTT, src/fft_2n.h:360-407).
+ *   - SYSTEMATIC encode: outputs = the m parities (codeword rows k..k+m-1).
+ *   - An output symbol equal to 65536 is stored as 0 and recorded as an
+ *     out-of-range (OOR) mark (src/fec_rs_fnt.h:253-269).
+ *
+ * Device layout: a *stripe* is a set of fragment rows of `words` u16 symbols.
+ * Row t of stripe s lives at base + s*stripe_stride + t*row_stride (strides in
+ * u16 elements).  One call processes n_stripes stripes; every column of every
+ * stripe is an independent codeword.
+ *
+ * OOR marks are kept in *buckets*: counts[s*slots + slot] (u32) and
+ * entries[(s*slots + slot)*cap + e] (u32 word offset within the row).  Encode
+ * zeroes nothing: callers clear counts (qi_gpu_oor_clear) before encoding.
+ * Entries inside a bucket are unordered; counts may exceed cap (overflow,
+ * detected by the caller).
+ */
+#ifndef QI_GPU_H
+#define QI_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct qi_plan qi_plan;
+
+/* Number of visible HIP devices (0 when none). */
+int qi_gpu_device_count(void);
+
+/* Create an RS-FNT plan (word_size 2 only).  Returns NULL on bad
+ * parameters (k < 1, m < 1, k+m > 65536) or when no device is present. */
+qi_plan* qi_plan_create(int k, int m, int systematic);
+void qi_plan_destroy(qi_plan* plan);
+/* n (FFT length) and n_outputs (m if systematic, k+m otherwise) */
+int qi_plan_n(const qi_plan* plan);
+int qi_plan_n_outputs(const qi_plan* plan);
+
+/* Zero n u32 OOR counters. */
+int qi_gpu_oor_clear(uint32_t* d_counts, size_t n, void* stream);
+
+/* Batch encode (device resident).  data: k rows per stripe.  out: n_outputs
+ * rows per stripe.  OOR buckets: slots = n_outputs, slot = output index.
+ * Pass d_oor_counts = NULL to skip OOR recording. */
+int qi_gpu_encode(qi_plan* plan, const uint16_t* d_data,
+                  long long data_stripe_stride, long long data_row_stride,
+                  uint16_t* d_out, long long out_stripe_stride,
+                  long long out_row_stride, long long words, int n_stripes,
+                  uint32_t* d_oor_counts, uint32_t* d_oor_entries, int oor_cap,
+                  void* stream);
+
+/* Bytes of device workspace for n_stripes decode contexts. */
+size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes);
+
+/* Build per-stripe decode contexts from the received fragment ids:
+ * d_ids[s*k + i] (u16, ascending, distinct, < k+m) -- the k fragments the
+ * decoder uses (FecCode::decode_blocks_vertical picks the first k present,
+ * src/fec_base.h:1199-1236).  k <= 64 on the device; larger k are built on
+ * the host from h_ids (may be NULL when k <= 64). */
+int qi_gpu_decode_ctx(qi_plan* plan, const uint16_t* d_ids,
+                      const uint16_t* h_ids, int n_stripes, void* d_ctx,
+                      void* stream);
+
+/* Batch decode.  Received fragment id f of stripe s is read from
+ *   f <  k (systematic data rows):  d_data + s*dss + f*drs
+ *   otherwise (coded row / parity): d_coded + s*css + slot*crs
+ * with slot = f - k (systematic) or f (non-systematic).
+ * OOR buckets of the coded rows are indexed by the same slot (slots =
+ * n_outputs); pass NULL counts when there are none.  Output: k data rows. */
+int qi_gpu_decode(qi_plan* plan, const void* d_ctx, const uint16_t* d_ids,
+                  const uint16_t* d_data, long long dss, long long drs,
+                  const uint16_t* d_coded, long long css, long long crs,
+                  const uint32_t* d_oor_counts, const uint32_t* d_oor_entries,
+                  int oor_cap, uint16_t* d_out, long long out_stripe_stride,
+                  long long out_row_stride, long long words, int n_stripes,
+                  void* stream);
+
+/* Non-zero if a decode overflowed its per-tile OOR scratch (sticky; reset
+ * by reading). Synchronous. */
+int qi_gpu_take_error(qi_plan* plan);
+
+
+/* ---- Block API over host buffers (C view of qi::fec::RsFnt, see
+ * include/qi_fec.hpp; semantics of FecCode::encode_blocks_vertical /
+ * decode_blocks_vertical, src/fec_base.h:1066-1321).  OOR marks are returned
+ * as per-output ascending offset lists of capacity oor_cap (counts exact). */
+typedef struct qi_fec qi_fec;
+qi_fec* qi_fec_new(int systematic, int k, int m);
+void qi_fec_delete(qi_fec* f);
+int qi_fec_n_outputs(const qi_fec* f);
+/* outputs: n_outputs pointers (NULL = not wanted). 0 or -1 */
+int qi_fec_encode_blocks(qi_fec* f, uint8_t** data, uint8_t** outputs,
+                         size_t block_bytes, uint32_t* oor, uint32_t* oor_count,
+                         uint32_t oor_cap);
+/* returns 1 decoded, 0 fewer than k fragments, -1 error */
+int qi_fec_decode_blocks(qi_fec* f, uint8_t** data, uint8_t** parities,
+                         const uint32_t* oor, const uint32_t* oor_count,
+                         uint32_t oor_cap, const int* missing,
+                         const int* wanted, size_t block_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,230 @@
+"""quadiron_amd -- MI355X-native RS-FNT erasure coding (Reed-Solomon over
+GF(65537) via the Fermat Number Transform), a drop-in for QuadIron's RS-FNT
+path.
+
+The product is the native library ``quadiron_amd/libquadiron_amd.so`` (HIP
+kernels for gfx950 + C++ host layer) exporting:
+
+* the drop-in C-ABI ``quadiron_fnt32_*`` (include/quadiron_c.h),
+* the device-level C-ABI ``qi_plan_* / qi_gpu_*`` (include/qi_gpu.h),
+* the C view of the block API ``qi_fec_*`` (include/qi_gpu.h).
+
+This module only loads it with ctypes and wraps those entry points for
+Python callers (tests, bench).  There is no Python or CPU compute path: if
+the library or a HIP device is missing, calls fail loudly.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libquadiron_amd.so")
+
+_lib = None
+
+c_u8p = C.POINTER(C.c_uint8)
+c_u8pp = C.POINTER(c_u8p)
+
+
+def _declare(lib):
+    V, I, LL, SZ, U32 = C.c_void_p, C.c_int, C.c_longlong, C.c_size_t, C.c_uint32
+    sig = {
+        # include/quadiron_c.h
+        "quadiron_fnt32_new": (V, [I, I, I, I]),
+        "quadiron_fnt32_delete": (None, [V]),
+        "quadiron_fnt32_get_metadata_size": (I, [V, SZ]),
+        "quadiron_fnt32_encode": (I, [V, c_u8pp, c_u8pp, V, SZ]),
+        "quadiron_fnt32_decode": (I, [V, c_u8pp, c_u8pp, V, SZ]),
+        "quadiron_fnt32_reconstruct": (I, [V, c_u8pp, c_u8pp, V, C.c_uint, SZ]),
+        "quadiron_hex_dump": (None, [V, SZ]),
+        # include/qi_gpu.h
+        "qi_gpu_device_count": (I, []),
+        "qi_plan_create": (V, [I, I, I]),
+        "qi_plan_destroy": (None, [V]),
+        "qi_plan_n": (I, [V]),
+        "qi_plan_n_outputs": (I, [V]),
+        "qi_gpu_oor_clear": (I, [V, SZ, V]),
+        "qi_gpu_encode": (I, [V, V, LL, LL, V, LL, LL, LL, I, V, V, I, V]),
+        "qi_gpu_decode_ctx_bytes": (SZ, [V, I]),
+        "qi_gpu_decode_ctx": (I, [V, V, V, I, V, V]),
+        "qi_gpu_decode": (I, [V, V, V, V, LL, LL, V, LL, LL, V, V, I, V, LL,
+                              LL, LL, I, V]),
+        "qi_gpu_take_error": (I, [V]),
+        "qi_fec_new": (V, [I, I, I]),
+        "qi_fec_delete": (None, [V]),
+        "qi_fec_n_outputs": (I, [V]),
+        "qi_fec_encode_blocks": (I, [V, c_u8pp, c_u8pp, SZ, V, V, U32]),
+        "qi_fec_decode_blocks": (I, [V, c_u8pp, c_u8pp, V, V, U32, V, V, SZ]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def lib():
+    """Load the native library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} missing: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` or "
+                "`make -C quadiron_amd/csrc`")
+        # torch-rocm bundles its own libamdhip64 with the same SONAME
+        # (libamdhip64.so.7): load torch first so the process keeps ONE HIP
+        # runtime (ours then binds to it) and torch streams/pointers are
+        # valid in our launches.  C-ABI users without torch get /opt/rocm's.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        _lib = _declare(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def require_device():
+    n = lib().qi_gpu_device_count()
+    if n < 1:
+        raise RuntimeError("quadiron_amd: no HIP device visible")
+    return n
+
+
+def ptr_array(arrs):
+    """uint8_t** from a list of numpy uint8 arrays (None -> NULL)."""
+    p = (c_u8p * len(arrs))()
+    for i, a in enumerate(arrs):
+        p[i] = a.ctypes.data_as(c_u8p) if a is not None else None
+    return p
+
+
+class Plan:
+    """Device plan (include/qi_gpu.h) for RS-FNT(k, m)."""
+
+    def __init__(self, k, m, systematic=False):
+        require_device()
+        self.k, self.m, self.sys = k, m, bool(systematic)
+        self.h = lib().qi_plan_create(k, m, int(systematic))
+        if not self.h:
+            raise ValueError(f"qi_plan_create({k}, {m}, {systematic}) failed")
+        self.n = lib().qi_plan_n(self.h)
+        self.n_outputs = lib().qi_plan_n_outputs(self.h)
+
+    def close(self):
+        if self.h:
+            lib().qi_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _stream(stream):
+        return stream if stream is not None else None
+
+    def encode(self, data, out, counts=None, entries=None, cap=0, stream=None):
+        """data: int16/uint16 tensor [S, k, P] on cuda; out: [S, n_out, P]."""
+        S, k, P = data.shape
+        assert k == self.k and out.shape[1] == self.n_outputs
+        rc = lib().qi_gpu_encode(
+            self.h, data.data_ptr(), data.stride(0), data.stride(1),
+            out.data_ptr(), out.stride(0), out.stride(1), P, S,
+            counts.data_ptr() if counts is not None else None,
+            entries.data_ptr() if entries is not None else None, int(cap),
+            self._stream(stream))
+        if rc:
+            raise RuntimeError(f"qi_gpu_encode failed: {rc}")
+
+    def ctx_bytes(self, n_stripes):
+        return lib().qi_gpu_decode_ctx_bytes(self.h, n_stripes)
+
+    def decode_ctx(self, ids, ctx, h_ids=None, stream=None):
+        """ids: int16 tensor [S, k] on cuda (fragment ids)."""
+        rc = lib().qi_gpu_decode_ctx(
+            self.h, ids.data_ptr(),
+            h_ids.ctypes.data_as(C.c_void_p) if h_ids is not None else None,
+            ids.shape[0], ctx.data_ptr(), self._stream(stream))
+        if rc:
+            raise RuntimeError(f"qi_gpu_decode_ctx failed: {rc}")
+
+    def decode(self, ctx, ids, coded, out, data=None, counts=None,
+               entries=None, cap=0, stream=None):
+        """coded: [S, n_out, P] (fragment slot rows); out: [S, k, P]."""
+        S, _, P = out.shape
+        d = data if data is not None else coded
+        rc = lib().qi_gpu_decode(
+            self.h, ctx.data_ptr(), ids.data_ptr(), d.data_ptr(), d.stride(0),
+            d.stride(1), coded.data_ptr(), coded.stride(0), coded.stride(1),
+            counts.data_ptr() if counts is not None else None,
+            entries.data_ptr() if entries is not None else None, int(cap),
+            out.data_ptr(), out.stride(0), out.stride(1), P, S,
+            self._stream(stream))
+        if rc:
+            raise RuntimeError(f"qi_gpu_decode failed: {rc}")
+        return lib().qi_gpu_take_error(self.h)
+
+
+class Fec:
+    """Block API (qi::fec::RsFnt via the qi_fec_* C view)."""
+
+    def __init__(self, k, m, systematic=False):
+        require_device()
+        self.k, self.m, self.sys = k, m, bool(systematic)
+        self.h = lib().qi_fec_new(int(systematic), k, m)
+        if not self.h:
+            raise ValueError("qi_fec_new failed")
+        self.n_outputs = lib().qi_fec_n_outputs(self.h)
+
+    def close(self):
+        if self.h:
+            lib().qi_fec_delete(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class QuadironFnt32:
+    """The drop-in C-ABI handle (include/quadiron_c.h)."""
+
+    def __init__(self, word_size, n_data, n_parities, systematic):
+        self.h = lib().quadiron_fnt32_new(word_size, n_data, n_parities,
+                                          int(systematic))
+        if not self.h:
+            raise ValueError("quadiron_fnt32_new returned NULL")
+        self.k, self.m, self.sys = n_data, n_parities, bool(systematic)
+
+    def metadata_size(self, block_size):
+        return lib().quadiron_fnt32_get_metadata_size(self.h, block_size)
+
+    def encode(self, data, parity, wanted, block_size):
+        return lib().quadiron_fnt32_encode(
+            self.h, ptr_array(data), ptr_array(parity),
+            wanted.ctypes.data_as(C.c_void_p), block_size)
+
+    def decode(self, data, parity, missing, block_size):
+        return lib().quadiron_fnt32_decode(
+            self.h, ptr_array(data), ptr_array(parity),
+            missing.ctypes.data_as(C.c_void_p), block_size)
+
+    def reconstruct(self, data, parity, missing, dest, block_size):
+        return lib().quadiron_fnt32_reconstruct(
+            self.h, ptr_array(data), ptr_array(parity),
+            missing.ctypes.data_as(C.c_void_p), dest, block_size)
+
+    def close(self):
+        if self.h:
+            lib().quadiron_fnt32_delete(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,617 @@
+// C++ FecCode-style API (include/qi_fec.hpp) on top of the device engine.
+//
+// The block/stream methods keep the reference's observable behaviour
+// (fragment selection, tail handling, OOR side channel, offsets) while the
+// per-packet loop of src/fec_base.h:1103-1150 becomes ONE device call over
+// the whole block: outputs do not depend on the packet size.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <arpa/inet.h>
+#include <chrono>
+#include <cstring>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/qi_fec.hpp"
+#include "../../include/qi_gpu.h"
+#include "qi_internal.h"
+#include "qi_plan.h"
+
+namespace qi {
+
+// ------------------------------------------------------------- Properties
+
+void Properties::sort()
+{
+    std::sort(props.begin(), props.end());
+}
+
+int Properties::fnt_serialize(uint32_t* dwords, unsigned n_dwords) const
+{
+    // src/property.h:104-118 (the last dword is left untouched)
+    if ((2 + props.size()) > n_dwords)
+        return -1;
+    dwords[0] = htonl(FNT1);
+    unsigned i = 2;
+    for (auto const& it : props)
+        dwords[i++] = htonl(static_cast<uint32_t>(it.first));
+    dwords[1] = htonl(i - 2);
+    for (unsigned d = i; d + 1 < n_dwords; d++)
+        dwords[d] = 0;
+    return 0;
+}
+
+int Properties::fnt_deserialize(const uint32_t* dwords, unsigned n_dwords)
+{
+    // src/property.h:125-142
+    if (n_dwords < 2)
+        return -1;
+    if (ntohl(dwords[0]) != FNT1)
+        return -1;
+    const uint32_t n = ntohl(dwords[1]);
+    if ((2 + static_cast<uint64_t>(n)) > n_dwords)
+        return -1;
+    for (uint32_t i = 0; i < n; i++)
+        add(static_cast<size_t>(ntohl(dwords[i + 2])), OOR_MARK);
+    return 0;
+}
+
+// text form of ec_driver's .props files (src/property.cpp:37-78)
+std::istream& operator>>(std::istream& is, Properties& p)
+{
+    std::string line;
+    while (std::getline(is, line)) {
+        auto b = line.find_first_not_of(" \f\t\v");
+        if (b == std::string::npos)
+            continue;
+        if (line[b] == '#' || line[b] == ';')
+            continue;
+        auto e = line.find('=', b);
+        std::string key = line.substr(b, e - b);
+        key.erase(key.find_last_not_of(" \f\t\v") + 1);
+        if (key.empty())
+            continue;
+        b = line.find_first_not_of(" \f\n\r\t\v", e + 1);
+        e = line.find_last_not_of(" \f\n\r\t\v") + 1;
+        p.add(std::stoul(key), static_cast<uint32_t>(std::stoul(line.substr(b, e - b))));
+    }
+    return is;
+}
+
+std::ostream& operator<<(std::ostream& os, const Properties& p)
+{
+    for (auto const& it : p.get_map())
+        os << it.first << " = " << it.second << '\n';
+    return os;
+}
+
+namespace fec {
+
+namespace {
+
+constexpr size_t kAlign = 64;  // row stride granule (u16 words)
+
+size_t pad_words(size_t w)
+{
+    return std::max<size_t>(kAlign, (w + kAlign - 1) / kAlign * kAlign);
+}
+
+void check(hipError_t e, const char* what)
+{
+    if (e != hipSuccess)
+        throw std::runtime_error(std::string("HIP error in ") + what + ": " +
+                                 hipGetErrorString(e));
+}
+
+void check_rc(int rc, const char* what)
+{
+    if (rc != 0)
+        throw std::runtime_error(std::string(what) + " failed: " +
+                                 std::to_string(rc));
+}
+
+struct Timer {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    uint64_t usec() const
+    {
+        return static_cast<uint64_t>(
+            std::chrono::duration_cast<std::chrono::microseconds>(
+                std::chrono::steady_clock::now() - t0)
+                .count());
+    }
+};
+
+}  // namespace
+
+RsFnt::RsFnt(FecType t, unsigned ws, unsigned k, unsigned m, size_t pkt)
+    : type(t), word_size(ws), n_data(k), n_parities(m), code_len(k + m),
+      n_outputs(t == FecType::SYSTEMATIC ? m : k + m), pkt_size(pkt),
+      buf_size(pkt * ws), n(0)
+{
+    if (ws != 2)
+        throw std::invalid_argument(
+            "RsFnt: only word_size 2 (GF(65537)) is supported");
+    if (k < 1 || m < 1 || pkt < 1)
+        throw std::invalid_argument("RsFnt: bad parameters");
+    plan_ = qi_plan_create(static_cast<int>(k), static_cast<int>(m),
+                           t == FecType::SYSTEMATIC ? 1 : 0);
+    if (!plan_)
+        throw std::runtime_error(
+            "RsFnt: cannot create the GPU plan (no HIP device or k > 128)");
+    n = static_cast<unsigned>(qi_plan_n(plan_));
+    check(hipStreamCreateWithFlags(&plan_->host.stream, hipStreamNonBlocking),
+          "hipStreamCreate");
+}
+
+RsFnt::~RsFnt()
+{
+    qi_plan_destroy(plan_);
+}
+
+int RsFnt::get_n_outputs() const
+{
+    // src/fec_rs_fnt.h:165-168
+    return type == FecType::SYSTEMATIC ? static_cast<int>(n_parities)
+                                       : static_cast<int>(n);
+}
+
+void RsFnt::encode_columns(const uint8_t* const* data, uint8_t* const* outputs,
+                           size_t words, std::vector<Properties>& props,
+                           size_t offset)
+{
+    if (words == 0)
+        return;
+    HostState& h = plan_->host;
+    hipStream_t s = h.stream;
+    const size_t P = pad_words(words);
+    const size_t no = n_outputs;
+    size_t cap = 64 + words / 512;
+    check(h.in.reserve(n_data * P * 2) ? hipSuccess : hipErrorOutOfMemory,
+          "alloc");
+    check(h.out.reserve(no * P * 2) ? hipSuccess : hipErrorOutOfMemory, "alloc");
+    check(h.counts.reserve(no * 4) ? hipSuccess : hipErrorOutOfMemory, "alloc");
+    uint16_t* din = static_cast<uint16_t*>(h.in.p);
+    uint16_t* dout = static_cast<uint16_t*>(h.out.p);
+    uint32_t* dcnt = static_cast<uint32_t*>(h.counts.p);
+    for (unsigned t = 0; t < n_data; t++)
+        check(hipMemcpyAsync(din + t * P, data[t], words * 2,
+                             hipMemcpyHostToDevice, s),
+              "H2D");
+    std::vector<uint32_t> cnt(no);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        check(h.entries.reserve(no * cap * 4) ? hipSuccess : hipErrorOutOfMemory,
+              "alloc");
+        check_rc(qi_gpu_oor_clear(dcnt, no, s), "oor_clear");
+        check_rc(qi_gpu_encode(plan_, din, 0, static_cast<long long>(P), dout, 0,
+                               static_cast<long long>(P),
+                               static_cast<long long>(words), 1, dcnt,
+                               static_cast<uint32_t*>(h.entries.p),
+                               static_cast<int>(cap), s),
+                 "qi_gpu_encode");
+        check(hipMemcpyAsync(cnt.data(), dcnt, no * 4, hipMemcpyDeviceToHost, s),
+              "D2H");
+        check(hipStreamSynchronize(s), "sync");
+        const uint32_t mx = *std::max_element(cnt.begin(), cnt.end());
+        if (mx <= cap)
+            break;
+        cap = mx;  // adversarial data: re-run with exact capacity
+    }
+    std::vector<uint32_t> ent(no * cap);
+    check(hipMemcpyAsync(ent.data(), h.entries.p, no * cap * 4,
+                         hipMemcpyDeviceToHost, s),
+          "D2H");
+    for (size_t i = 0; i < no; i++)
+        if (outputs[i])
+            check(hipMemcpyAsync(outputs[i], dout + i * P, words * 2,
+                                 hipMemcpyDeviceToHost, s),
+                  "D2H");
+    check(hipStreamSynchronize(s), "sync");
+    for (size_t i = 0; i < no; i++) {
+        uint32_t* b = ent.data() + i * cap;
+        std::sort(b, b + cnt[i]);
+        for (uint32_t e = 0; e < cnt[i]; e++)
+            props[i].add(offset + b[e], OOR_MARK);
+    }
+}
+
+void RsFnt::decode_columns(const std::vector<int>& ids,
+                           const std::vector<const uint8_t*>& rows,
+                           const std::vector<const Properties*>& props,
+                           uint8_t* const* outputs, size_t words,
+                           size_t offset)
+{
+    if (words == 0)
+        return;
+    HostState& h = plan_->host;
+    hipStream_t s = h.stream;
+    const size_t P = pad_words(words);
+    const int k = static_cast<int>(n_data);
+    // OOR marks of the received coded rows inside [offset, offset+words)
+    std::vector<std::vector<uint32_t>> marks(k);
+    size_t cap = 1;
+    for (int i = 0; i < k; i++) {
+        if (!props[i])
+            continue;
+        for (auto const& it : props[i]->get_map())
+            if (it.first >= offset && it.first < offset + words)
+                marks[i].push_back(static_cast<uint32_t>(it.first - offset));
+        cap = std::max(cap, marks[i].size());
+    }
+    std::vector<uint32_t> hcnt(k), hent(static_cast<size_t>(k) * cap, 0);
+    for (int i = 0; i < k; i++) {
+        hcnt[i] = static_cast<uint32_t>(marks[i].size());
+        std::copy(marks[i].begin(), marks[i].end(), hent.begin() + i * cap);
+    }
+    std::vector<uint16_t> hids(k);
+    for (int i = 0; i < k; i++)
+        hids[i] = static_cast<uint16_t>(ids[i]);
+    const size_t ctx_bytes = qi_gpu_decode_ctx_bytes(plan_, 1);
+    const size_t cnt_off = 0, ent_off = 64 * ((k * 4 + 63) / 64);
+    if (!h.in.reserve(static_cast<size_t>(k) * P * 2) ||
+        !h.out.reserve(static_cast<size_t>(k) * P * 2) ||
+        !h.counts.reserve(ent_off + hent.size() * 4) ||
+        !h.ids.reserve(k * 2) || !h.ctx.reserve(ctx_bytes))
+        throw std::runtime_error("RsFnt: device allocation failed");
+    uint16_t* din = static_cast<uint16_t*>(h.in.p);
+    uint16_t* dout = static_cast<uint16_t*>(h.out.p);
+    uint8_t* dcb = static_cast<uint8_t*>(h.counts.p);
+    for (int i = 0; i < k; i++)
+        check(hipMemcpyAsync(din + i * P, rows[i], words * 2,
+                             hipMemcpyHostToDevice, s),
+              "H2D");
+    check(hipMemcpyAsync(dcb + cnt_off, hcnt.data(), k * 4, hipMemcpyHostToDevice,
+                         s),
+          "H2D");
+    check(hipMemcpyAsync(dcb + ent_off, hent.data(), hent.size() * 4,
+                         hipMemcpyHostToDevice, s),
+          "H2D");
+    check(hipMemcpyAsync(h.ids.p, hids.data(), k * 2, hipMemcpyHostToDevice, s),
+          "H2D");
+    check_rc(qi_gpu_decode_ctx(plan_, static_cast<uint16_t*>(h.ids.p),
+                               hids.data(), 1, h.ctx.p, s),
+             "qi_gpu_decode_ctx");
+    // received rows staged by position; OOR buckets by position
+    const MatLayout L{k, k, matrix_kp(k)};
+    RowSrc src{din, 0, static_cast<long long>(P), 1 << 30, nullptr, 0, 0, 1};
+    RowDst dst{dout, 0, static_cast<long long>(P)};
+    Oor in{reinterpret_cast<uint32_t*>(dcb + cnt_off),
+           reinterpret_cast<uint32_t*>(dcb + ent_off), k,
+           static_cast<int>(cap)};
+    check_rc(launch_matrix(L, static_cast<const int32_t*>(h.ctx.p), 0,
+                           static_cast<uint16_t*>(h.ids.p), src, dst,
+                           static_cast<long long>(words), 1, &in, 0, nullptr,
+                           plan_->d_err, s),
+             "decode");
+    for (int t = 0; t < k; t++)
+        if (outputs[t])
+            check(hipMemcpyAsync(outputs[t], dout + t * P, words * 2,
+                                 hipMemcpyDeviceToHost, s),
+                  "D2H");
+    check(hipStreamSynchronize(s), "sync");
+    if (qi_gpu_take_error(plan_))
+        throw std::runtime_error("RsFnt: too many OOR marks in one tile");
+}
+
+void RsFnt::encode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
+                                   std::vector<uint8_t*>& parities_bufs,
+                                   std::vector<Properties>& parities_props,
+                                   std::vector<bool>& wanted_idxs,
+                                   size_t block_size_bytes)
+{
+    // src/fec_base.h:1066-1151
+    for (auto& p : parities_props)
+        p.clear();
+    reset_stats_enc();
+    const size_t words = block_size_bytes / word_size;
+    std::vector<uint8_t*> outs(n_outputs, nullptr);
+    for (unsigned i = 0; i < n_outputs; i++)
+        if (wanted_idxs[i])
+            outs[i] = parities_bufs[i];
+    Timer tm;
+    encode_columns(data_bufs.data(), outs.data(), words, parities_props, 0);
+    total_enc_usec += tm.usec();
+    n_encode_ops++;
+}
+
+bool RsFnt::select_fragments(const std::vector<int>& present,
+                             std::vector<int>& ids) const
+{
+    // first k present, data before parities: src/fec_base.h:1199-1236
+    ids.clear();
+    const bool sys = type == FecType::SYSTEMATIC;
+    if (sys)
+        for (unsigned i = 0; i < n_data; i++)
+            if (present[i])
+                ids.push_back(static_cast<int>(i));
+    for (unsigned i = 0; i < n_outputs && ids.size() < n_data; i++) {
+        const unsigned j = sys ? n_data + i : i;
+        if (present[j])
+            ids.push_back(static_cast<int>(j));
+    }
+    return ids.size() == n_data;
+}
+
+bool RsFnt::decode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
+                                   std::vector<uint8_t*>& parities_bufs,
+                                   std::vector<Properties>& parities_props,
+                                   std::vector<int>& missing_idxs,
+                                   std::vector<bool>& wanted_idxs,
+                                   size_t block_size_bytes)
+{
+    // src/fec_base.h:1177-1321
+    const bool sys = type == FecType::SYSTEMATIC;
+    std::vector<int> present(code_len);
+    for (unsigned i = 0; i < code_len; i++)
+        present[i] = missing_idxs[i] ? 0 : 1;
+    if (sys) {
+        unsigned nd = 0;
+        for (unsigned i = 0; i < n_data; i++)
+            nd += present[i];
+        if (nd == n_data)
+            return true;  // data in clear (src/fec_base.h:1208-1211)
+    }
+    std::vector<int> ids;
+    if (!select_fragments(present, ids))
+        return false;
+    // DecodeContext sorts every input property list (src/fec_context.h:93-97)
+    for (auto& p : parities_props)
+        p.sort();
+    reset_stats_dec();
+    std::vector<const uint8_t*> rows(n_data);
+    std::vector<const Properties*> props(n_data, nullptr);
+    for (unsigned i = 0; i < n_data; i++) {
+        const int id = ids[i];
+        if (sys && id < static_cast<int>(n_data)) {
+            rows[i] = data_bufs[id];
+        } else {
+            const int slot = sys ? id - static_cast<int>(n_data) : id;
+            rows[i] = parities_bufs[slot];
+            props[i] = &parities_props[slot];
+        }
+    }
+    std::vector<uint8_t*> outs(n_data, nullptr);
+    for (unsigned t = 0; t < n_data; t++)
+        if (wanted_idxs[t])
+            outs[t] = data_bufs[t];
+    Timer tm;
+    decode_columns(ids, rows, props, outs.data(), block_size_bytes / word_size, 0);
+    total_dec_usec += tm.usec();
+    n_decode_ops++;
+    return true;
+}
+
+namespace {
+
+size_t chunk_bytes(size_t buf_size)
+{
+    const size_t target = 8u << 20;
+    return buf_size * std::max<size_t>(1, target / buf_size);
+}
+
+// read up to `len` bytes; returns bytes read (short = end of stream)
+size_t read_full(std::istream* is, uint8_t* p, size_t len)
+{
+    is->read(reinterpret_cast<char*>(p), static_cast<std::streamsize>(len));
+    return static_cast<size_t>(is->gcount());
+}
+
+}  // namespace
+
+void RsFnt::encode_streams_vertical(
+    const std::vector<std::istream*>& input_data_bufs,
+    std::vector<std::ostream*>& output_parities_bufs,
+    std::vector<Properties>& output_parities_props)
+{
+    // src/fec_base.h:463-542: packets of buf_size bytes, zero padded tail,
+    // `read_bytes` of every output written for the last packet
+    for (auto& p : output_parities_props)
+        p.clear();
+    reset_stats_enc();
+    const size_t CH = chunk_bytes(buf_size);
+    std::vector<std::vector<uint8_t>> in(n_data, std::vector<uint8_t>(CH + 2));
+    std::vector<std::vector<uint8_t>> out(n_outputs, std::vector<uint8_t>(CH + 2));
+    size_t offset = 0;
+    bool cont = true;
+    while (cont) {
+        size_t got = CH;
+        for (unsigned i = 0; i < n_data; i++) {
+            const size_t r = read_full(input_data_bufs[i], in[i].data(), CH);
+            if (r < CH) {
+                got = r;
+                cont = false;
+            }
+        }
+        if (got == 0)
+            break;
+        for (unsigned i = 0; i < n_data; i++)
+            std::fill(in[i].begin() + got, in[i].end(), 0);
+        std::vector<const uint8_t*> dp(n_data);
+        std::vector<uint8_t*> op(n_outputs);
+        for (unsigned i = 0; i < n_data; i++)
+            dp[i] = in[i].data();
+        for (unsigned i = 0; i < n_outputs; i++)
+            op[i] = out[i].data();
+        Timer tm;
+        encode_columns(dp.data(), op.data(), (got + 1) / 2, output_parities_props,
+                       offset);
+        total_enc_usec += tm.usec();
+        n_encode_ops++;
+        for (unsigned i = 0; i < n_outputs; i++)
+            output_parities_bufs[i]->write(reinterpret_cast<char*>(out[i].data()),
+                                           static_cast<std::streamsize>(got));
+        offset += got / 2;
+    }
+}
+
+bool RsFnt::decode_streams_vertical(
+    const std::vector<std::istream*>& input_data_bufs,
+    const std::vector<std::istream*>& input_parities_bufs,
+    std::vector<Properties>& input_parities_props,
+    std::vector<std::ostream*>& output_data_bufs)
+{
+    // src/fec_base.h:898-1048
+    const bool sys = type == FecType::SYSTEMATIC;
+    std::vector<int> present(code_len, 0);
+    if (sys)
+        for (unsigned i = 0; i < n_data; i++)
+            present[i] = input_data_bufs[i] != nullptr;
+    for (unsigned i = 0; i < n_outputs; i++)
+        present[sys ? n_data + i : i] = input_parities_bufs[i] != nullptr;
+    if (sys) {
+        unsigned nd = 0;
+        for (unsigned i = 0; i < n_data; i++)
+            nd += present[i];
+        if (nd == n_data)
+            return true;
+    }
+    std::vector<int> ids;
+    if (!select_fragments(present, ids))
+        return false;
+    for (auto& p : input_parities_props)
+        p.sort();
+    reset_stats_dec();
+    std::vector<std::istream*> src(n_data);
+    std::vector<const Properties*> props(n_data, nullptr);
+    for (unsigned i = 0; i < n_data; i++) {
+        const int id = ids[i];
+        if (sys && id < static_cast<int>(n_data)) {
+            src[i] = input_data_bufs[id];
+        } else {
+            const int slot = sys ? id - static_cast<int>(n_data) : id;
+            src[i] = input_parities_bufs[slot];
+            props[i] = &input_parities_props[slot];
+        }
+    }
+    const size_t CH = chunk_bytes(buf_size);
+    std::vector<std::vector<uint8_t>> in(n_data, std::vector<uint8_t>(CH + 2));
+    std::vector<std::vector<uint8_t>> out(n_data, std::vector<uint8_t>(CH + 2));
+    size_t offset = 0;
+    bool cont = true;
+    while (cont) {
+        size_t got = CH;
+        for (unsigned i = 0; i < n_data; i++) {
+            const size_t r = read_full(src[i], in[i].data(), CH);
+            if (r < CH) {
+                got = r;
+                cont = false;
+            }
+        }
+        if (got == 0)
+            break;
+        for (unsigned i = 0; i < n_data; i++)
+            std::fill(in[i].begin() + got, in[i].end(), 0);
+        std::vector<const uint8_t*> rp(n_data);
+        std::vector<uint8_t*> op(n_data);
+        for (unsigned i = 0; i < n_data; i++) {
+            rp[i] = in[i].data();
+            op[i] = output_data_bufs[i] ? out[i].data() : nullptr;
+        }
+        Timer tm;
+        decode_columns(ids, rp, props, op.data(), (got + 1) / 2, offset);
+        total_dec_usec += tm.usec();
+        n_decode_ops++;
+        for (unsigned i = 0; i < n_data; i++)
+            if (output_data_bufs[i])
+                output_data_bufs[i]->write(reinterpret_cast<char*>(out[i].data()),
+                                           static_cast<std::streamsize>(got));
+        offset += got / 2;
+    }
+    return true;
+}
+
+}  // namespace fec
+}  // namespace qi
+
+// ---------------------------------------------------------------- C view
+
+struct qi_fec {
+    qi::fec::RsFnt* f;
+};
+
+extern "C" {
+
+qi_fec* qi_fec_new(int systematic, int k, int m)
+{
+    try {
+        auto* h = new qi_fec;
+        h->f = new qi::fec::RsFnt(systematic ? qi::fec::FecType::SYSTEMATIC
+                                             : qi::fec::FecType::NON_SYSTEMATIC,
+                                  2, static_cast<unsigned>(k),
+                                  static_cast<unsigned>(m), 1024);
+        return h;
+    } catch (...) {
+        return nullptr;
+    }
+}
+
+void qi_fec_delete(qi_fec* h)
+{
+    if (h) {
+        delete h->f;
+        delete h;
+    }
+}
+
+int qi_fec_n_outputs(const qi_fec* h)
+{
+    return h ? static_cast<int>(h->f->n_outputs) : -1;
+}
+
+int qi_fec_encode_blocks(qi_fec* h, uint8_t** data, uint8_t** outputs,
+                         size_t block_bytes, uint32_t* oor, uint32_t* oor_count,
+                         uint32_t cap)
+{
+    try {
+        qi::fec::RsFnt& f = *h->f;
+        std::vector<uint8_t*> dv(data, data + f.n_data);
+        std::vector<uint8_t*> pv(outputs, outputs + f.n_outputs);
+        std::vector<qi::Properties> props(f.n_outputs);
+        std::vector<bool> wanted(f.n_outputs);
+        for (unsigned i = 0; i < f.n_outputs; i++)
+            wanted[i] = outputs[i] != nullptr;
+        f.encode_blocks_vertical(dv, pv, props, wanted, block_bytes);
+        for (unsigned i = 0; i < f.n_outputs; i++) {
+            uint32_t c = 0;
+            for (auto const& it : props[i].get_map()) {
+                if (c < cap)
+                    oor[static_cast<size_t>(i) * cap + c] =
+                        static_cast<uint32_t>(it.first);
+                c++;
+            }
+            oor_count[i] = c;
+        }
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
+int qi_fec_decode_blocks(qi_fec* h, uint8_t** data, uint8_t** parities,
+                         const uint32_t* oor, const uint32_t* oor_count,
+                         uint32_t cap, const int* missing, const int* wanted,
+                         size_t block_bytes)
+{
+    try {
+        qi::fec::RsFnt& f = *h->f;
+        std::vector<uint8_t*> dv(data, data + f.n_data);
+        std::vector<uint8_t*> pv(parities, parities + f.n_outputs);
+        std::vector<qi::Properties> props(f.n_outputs);
+        for (unsigned i = 0; i < f.n_outputs; i++) {
+            const uint32_t c = oor_count[i] < cap ? oor_count[i] : cap;
+            for (uint32_t e = 0; e < c; e++)
+                props[i].add(oor[static_cast<size_t>(i) * cap + e], qi::OOR_MARK);
+        }
+        std::vector<int> miss(missing, missing + f.code_len);
+        std::vector<bool> want(f.n_data);
+        for (unsigned i = 0; i < f.n_data; i++)
+            want[i] = wanted[i] != 0;
+        return f.decode_blocks_vertical(dv, pv, props, miss, want, block_bytes) ? 1
+                                                                                : 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,183 @@
+// Plan construction and host-side matrix math for the RS-FNT engine.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/qi_gpu.h"
+#include "gf65537.h"
+#include "matrix_pack.h"
+#include "qi_internal.h"
+#include "qi_plan.h"
+
+namespace qi {
+
+static uint32_t addm(uint32_t a, uint32_t b)
+{
+    const uint32_t c = a + b;
+    return c >= 65537u ? c - 65537u : c;
+}
+static uint32_t subm(uint32_t a, uint32_t b)
+{
+    return a >= b ? a - b : a + 65537u - b;
+}
+
+// Lagrange basis for points x_i = r^{ids[i]} (the closed form of the
+// interpolation performed by FecCode::decode_apply, src/fec_base.h:682-738).
+std::vector<uint32_t> lagrange_matrix(int k, uint32_t r, const uint32_t* ids,
+                                      int mode, const uint32_t* eval, int R)
+{
+    std::vector<uint32_t> x(k), A(k + 1, 0), q(k), M(static_cast<size_t>(R) * k);
+    for (int i = 0; i < k; i++)
+        x[i] = powmod_c(r, ids[i]);
+    A[0] = 1;
+    for (int i = 0; i < k; i++) {
+        const uint32_t neg = subm(0, x[i]);
+        A[i + 1] = A[i];
+        for (int d = i; d > 0; d--)
+            A[d] = addm(A[d - 1], mulmod_c(A[d], neg));
+        A[0] = mulmod_c(A[0], neg);
+    }
+    for (int i = 0; i < k; i++) {
+        q[k - 1] = A[k];
+        for (int j = k - 1; j >= 1; j--)
+            q[j - 1] = addm(A[j], mulmod_c(x[i], q[j]));
+        uint32_t den = 1;
+        for (int j = 0; j < k; j++)
+            if (j != i)
+                den = mulmod_c(den, subm(x[i], x[j]));
+        const uint32_t inv = invmod_c(den);
+        for (int t = 0; t < R; t++) {
+            uint32_t v;
+            if (mode == 0) {
+                v = q[t];
+            } else {
+                v = 0;
+                for (int j = k - 1; j >= 0; j--)
+                    v = addm(mulmod_c(v, eval[t]), q[j]);
+            }
+            M[static_cast<size_t>(t) * k + i] = mulmod_c(v, inv);
+        }
+    }
+    return M;
+}
+
+void pack_matrix(const MatLayout& L, const uint32_t* M, int32_t* block)
+{
+    std::memset(block, 0, L.words() * sizeof(int32_t));
+    for (int t = 0; t < L.R; t++)
+        pack_row(M + static_cast<size_t>(t) * L.kin, L.kin, L.KP, L.R, t, block);
+}
+
+}  // namespace qi
+
+using namespace qi;
+
+extern "C" {
+
+int qi_gpu_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n;
+}
+
+qi_plan* qi_plan_create(int k, int m, int systematic)
+{
+    if (k < 1 || m < 1 || k + m > 65536 || 2 * k >= 65537)
+        return nullptr;
+    if (qi_gpu_device_count() < 1)
+        return nullptr;
+    qi_plan* p = new (std::nothrow) qi_plan();
+    if (!p)
+        return nullptr;
+    p->k = k;
+    p->m = m;
+    p->sys = systematic ? 1 : 0;
+    p->code_len = k + m;
+    p->n_outputs = p->sys ? m : k + m;
+    p->n = static_cast<int>(ceil2(static_cast<uint32_t>(k + m)));
+    p->K = static_cast<int>(ceil2(static_cast<uint32_t>(k)));
+    p->r = root_of_unity(static_cast<uint32_t>(p->n));
+    (void)hipGetDevice(&p->device);
+
+    bool ok = true;
+    // twist factors w^{v t} for the encode passes (K <= 64)
+    if (!p->sys && p->K <= 64) {
+        const int passes = p->n / p->K;
+        std::vector<int32_t> tw(static_cast<size_t>(passes) * p->K);
+        for (int v = 0; v < passes; v++)
+            for (int t = 0; t < p->K; t++)
+                tw[static_cast<size_t>(v) * p->K + t] = balanced(powmod_c(
+                    p->r, static_cast<uint32_t>((static_cast<long long>(v) * t) % p->n)));
+        ok = ok && hipMalloc(&p->d_twist, tw.size() * 4) == hipSuccess &&
+             hipMemcpy(p->d_twist, tw.data(), tw.size() * 4,
+                       hipMemcpyHostToDevice) == hipSuccess;
+    }
+    // generator matrix for the systematic encode or for a non-systematic
+    // encode too wide for the register codelets: outputs x inputs
+    const int kp = matrix_kp(k);
+    if (kp < 0) {
+        ok = false;  // k > 64 is not supported by the matrix kernel
+    } else if (p->sys || p->K > 64) {
+        MatLayout L{p->n_outputs, k, kp};
+        std::vector<uint32_t> M;
+        if (p->sys) {
+            std::vector<uint32_t> ids(k), ev(m);
+            for (int i = 0; i < k; i++)
+                ids[i] = static_cast<uint32_t>(i);
+            for (int i = 0; i < m; i++)
+                ev[i] = powmod_c(p->r, static_cast<uint32_t>(k + i));
+            // parity i = P(r^{k+i}) where P interpolates data at r^0..r^{k-1}
+            // (src/fec_rs_fnt.h:204-251 SYSTEMATIC branch)
+            M = lagrange_matrix(k, p->r, ids.data(), 1, ev.data(), m);
+        } else {
+            M.resize(static_cast<size_t>(p->n_outputs) * k);
+            for (int i = 0; i < p->n_outputs; i++)
+                for (int t = 0; t < k; t++)
+                    M[static_cast<size_t>(i) * k + t] = powmod_c(
+                        p->r, static_cast<uint32_t>((static_cast<long long>(i) * t) % p->n));
+        }
+        std::vector<int32_t> blk(L.words());
+        pack_matrix(L, M.data(), blk.data());
+        p->gen = L;
+        ok = ok && hipMalloc(&p->d_gen, blk.size() * 4) == hipSuccess &&
+             hipMemcpy(p->d_gen, blk.data(), blk.size() * 4,
+                       hipMemcpyHostToDevice) == hipSuccess;
+    }
+    ok = ok && hipMalloc(&p->d_err, 4) == hipSuccess &&
+         hipMemset(p->d_err, 0, 4) == hipSuccess;
+    if (!ok) {
+        qi_plan_destroy(p);
+        return nullptr;
+    }
+    return p;
+}
+
+void qi_plan_destroy(qi_plan* p)
+{
+    if (!p)
+        return;
+    if (p->d_twist)
+        (void)hipFree(p->d_twist);
+    if (p->d_gen)
+        (void)hipFree(p->d_gen);
+    if (p->d_err)
+        (void)hipFree(p->d_err);
+    p->host.release();
+    delete p;
+}
+
+int qi_plan_n(const qi_plan* p)
+{
+    return p ? p->n : -1;
+}
+
+int qi_plan_n_outputs(const qi_plan* p)
+{
+    return p ? p->n_outputs : -1;
+}
+
+}  // extern "C"

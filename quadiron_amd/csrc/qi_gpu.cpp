@@ -1,0 +1,142 @@
+// Device-level C-ABI (include/qi_gpu.h): batch encode / decode on
+// device-resident stripes.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../../include/qi_gpu.h"
+#include "gf65537.h"
+#include "qi_internal.h"
+#include "qi_plan.h"
+
+using namespace qi;
+
+namespace {
+
+MatLayout ctx_layout(const qi_plan* p)
+{
+    return MatLayout{p->k, p->k, matrix_kp(p->k)};
+}
+
+hipStream_t st(void* s)
+{
+    return static_cast<hipStream_t>(s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int qi_gpu_oor_clear(uint32_t* d_counts, size_t n, void* stream)
+{
+    if (!d_counts || n == 0)
+        return 0;
+    return hipMemsetAsync(d_counts, 0, n * sizeof(uint32_t), st(stream)) ==
+                   hipSuccess
+               ? 0
+               : -2;
+}
+
+int qi_gpu_encode(qi_plan* p, const uint16_t* d_data, long long dss,
+                  long long drs, uint16_t* d_out, long long oss, long long ors,
+                  long long words, int n_stripes, uint32_t* d_counts,
+                  uint32_t* d_entries, int cap, void* stream)
+{
+    if (!p || !d_data || !d_out || n_stripes < 0 || words < 0)
+        return -1;
+    if (n_stripes == 0 || words == 0)
+        return 0;
+    Oor oor{d_counts, d_entries, p->n_outputs, cap};
+    RowDst out{d_out, oss, ors};
+    if (!p->sys && p->K <= 64)
+        return launch_encode_fnt(p->k, p->n, p->n_outputs, p->d_twist, d_data,
+                                 dss, drs, out, words, n_stripes, oor,
+                                 p->d_err, st(stream));
+    RowSrc src{d_data, dss, drs, 1 << 30, nullptr, 0, 0, 0};
+    return launch_matrix(p->gen, p->d_gen, 0, nullptr, src, out, words,
+                         n_stripes, nullptr, 0, d_counts ? &oor : nullptr,
+                         p->d_err, st(stream));
+}
+
+size_t qi_gpu_decode_ctx_bytes(const qi_plan* p, int n_stripes)
+{
+    if (!p || n_stripes < 0)
+        return 0;
+    return ctx_layout(p).words() * sizeof(int32_t) *
+           static_cast<size_t>(n_stripes);
+}
+
+int qi_gpu_decode_ctx(qi_plan* p, const uint16_t* d_ids,
+                      const uint16_t* h_ids, int n_stripes, void* d_ctx,
+                      void* stream)
+{
+    if (!p || !d_ctx || n_stripes < 0)
+        return -1;
+    if (n_stripes == 0)
+        return 0;
+    const MatLayout L = ctx_layout(p);
+    if (L.KP < 0)
+        return -3;
+    const int mode = p->sys ? 1 : 0;
+    if (p->k <= 64 && d_ids)
+        return launch_decode_ctx(p->k, p->n, p->r, mode, L, d_ids, n_stripes,
+                                 static_cast<int32_t*>(d_ctx), st(stream));
+    if (!h_ids)
+        return -1;
+    // host build (k > 64): same Lagrange form as the device kernel
+    std::vector<int32_t> blk(L.words() * static_cast<size_t>(n_stripes));
+    std::vector<uint32_t> ids(p->k), ev(p->k);
+    for (int t = 0; t < p->k; t++)
+        ev[t] = qi::powmod_c(p->r, static_cast<uint32_t>(t));
+    for (int s = 0; s < n_stripes; s++) {
+        for (int i = 0; i < p->k; i++)
+            ids[i] = h_ids[static_cast<size_t>(s) * p->k + i];
+        std::vector<uint32_t> M =
+            lagrange_matrix(p->k, p->r, ids.data(), mode, ev.data(), p->k);
+        pack_matrix(L, M.data(), blk.data() + L.words() * s);
+    }
+    if (hipMemcpyAsync(d_ctx, blk.data(), blk.size() * 4, hipMemcpyHostToDevice,
+                       st(stream)) != hipSuccess)
+        return -2;
+    return hipStreamSynchronize(st(stream)) == hipSuccess ? 0 : -2;
+}
+
+int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
+                  const uint16_t* d_data, long long dss, long long drs,
+                  const uint16_t* d_coded, long long css, long long crs,
+                  const uint32_t* d_counts, const uint32_t* d_entries, int cap,
+                  uint16_t* d_out, long long oss, long long ors,
+                  long long words, int n_stripes, void* stream)
+{
+    if (!p || !d_ctx || !d_ids || !d_out || !d_coded || n_stripes < 0)
+        return -1;
+    if (n_stripes == 0 || words == 0)
+        return 0;
+    const MatLayout L = ctx_layout(p);
+    RowSrc src;
+    if (p->sys)
+        src = RowSrc{d_data ? d_data : d_coded, dss, drs, p->k, d_coded, css, crs, 0};
+    else
+        src = RowSrc{d_coded, css, crs, 1 << 30, nullptr, 0, 0, 0};
+    Oor in{const_cast<uint32_t*>(d_counts), const_cast<uint32_t*>(d_entries),
+           p->n_outputs, cap};
+    RowDst out{d_out, oss, ors};
+    return launch_matrix(L, static_cast<const int32_t*>(d_ctx),
+                         static_cast<long long>(L.words()), d_ids, src, out,
+                         words, n_stripes, d_counts ? &in : nullptr,
+                         p->sys ? p->k : 0, nullptr, p->d_err, st(stream));
+}
+
+int qi_gpu_take_error(qi_plan* p)
+{
+    if (!p)
+        return -1;
+    uint32_t e = 0;
+    if (hipMemcpy(&e, p->d_err, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return -2;
+    if (e)
+        (void)hipMemset(p->d_err, 0, 4);
+    return static_cast<int>(e);
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// Internal (host-side) declarations shared by the plan, the device shim and
+// the drop-in C-ABI.  Nothing here crosses the public C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+namespace qi {
+
+// Packed interpolation / generator matrix block, one per stripe (or shared).
+//   packed[R][KP]  int16 pairs (balanced, |c| <= 32766) of the row-scaled
+//                  matrix, zero padded past kin
+//   kcorr[R]       32768 * sum_i c[t][i] mod q (undoes the x - 32768 offset)
+//   rscale[R]      balanced inverse row scale (1 = unscaled)
+//   plain[R][kin]  canonical row-scaled entries (OOR corrections)
+struct MatLayout {
+    int R, kin, KP;
+    __host__ __device__ size_t packed() const { return 0; }
+    __host__ __device__ size_t kcorr() const { return static_cast<size_t>(R) * KP; }
+    __host__ __device__ size_t rscale() const { return kcorr() + R; }
+    __host__ __device__ size_t plain() const { return rscale() + R; }
+    __host__ __device__ size_t words() const { return plain() + static_cast<size_t>(R) * kin; }
+};
+
+// Row source for the matrix kernel: fragment `id` of stripe `s` is at
+//   id <  split : base0 + s*ss0 + id*rs0
+//   id >= split : base1 + s*ss1 + (id-split)*rs1        (elements of u16)
+//   by_pos != 0: row (and OOR slot) of the i-th received fragment is found
+//   by its position i instead of its id (compact staging of the block API)
+struct RowSrc {
+    const uint16_t* base0;
+    long long ss0, rs0;
+    int split;
+    const uint16_t* base1;
+    long long ss1, rs1;
+    int by_pos;
+};
+
+// Output rows: row t of stripe s at base + s*ss + t*rs
+struct RowDst {
+    uint16_t* base;
+    long long ss, rs;
+};
+
+// OOR buckets: counts[s*slots + slot], entries[(s*slots + slot)*cap + e]
+struct Oor {
+    uint32_t* counts;
+    uint32_t* entries;
+    int slots;
+    int cap;
+};
+
+// ---- launchers (kernels.hip) ----
+// non-systematic encode by twisted register-resident sub-NTTs
+int launch_encode_fnt(int k, int n, int n_out, const int32_t* d_twist,
+                      const uint16_t* data, long long dss, long long drs,
+                      RowDst out, long long words, int n_stripes, Oor oor,
+                      uint32_t* d_err, hipStream_t stream);
+
+// out[t] = sum_i M[t][i] * in[ids[i]]  for t < R
+//   mat: per-stripe blocks (mat_stride words apart; 0 = shared)
+//   ids: S x kin fragment ids (nullptr = identity 0..kin-1)
+//   in_oor: restore buckets by slot (nullptr = none); slot_of_id = id -
+//     slot_base (ids < slot_base have no bucket)
+//   out_oor: record OOR outputs (nullptr = no recording; values stored as 0)
+int launch_matrix(const MatLayout& L, const int32_t* mat, long long mat_stride,
+                  const uint16_t* ids, RowSrc src, RowDst dst, long long words,
+                  int n_stripes, const Oor* in_oor, int slot_base,
+                  const Oor* out_oor, uint32_t* d_err, hipStream_t stream);
+
+// per-stripe decode matrices from fragment ids (S x k).
+//   mode 0: coefficient extraction (non-systematic: data = poly coefs)
+//   mode 1: evaluation at r^t, t < k (systematic: data = P(r^t))
+int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
+                      const uint16_t* d_ids, int n_stripes, int32_t* d_mat,
+                      hipStream_t stream);
+
+// matrix kernel instantiation choice
+int matrix_kp(int kin);
+
+// ---- host math (plan.cpp) ----
+// Lagrange matrix for points x_i = r^{ids[i]}:
+//   mode 0: M[t][i] = coef_t(L_i), t < k
+//   mode 1: M[t][i] = L_i(eval[t]), t < R
+std::vector<uint32_t> lagrange_matrix(int k, uint32_t r, const uint32_t* ids,
+                                      int mode, const uint32_t* eval, int R);
+// pack a canonical R x kin matrix into a MatLayout block
+void pack_matrix(const MatLayout& L, const uint32_t* M, int32_t* block);
+
+}  // namespace qi

@@ -1,0 +1,69 @@
+// The opaque qi_plan behind include/qi_gpu.h (host-only definition).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "qi_internal.h"
+
+namespace qi {
+
+// grow-only device scratch owned by a plan (block API staging)
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    bool reserve(size_t n)
+    {
+        if (n <= bytes)
+            return true;
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, n) != hipSuccess) {
+            p = nullptr;
+            return false;
+        }
+        bytes = n;
+        return true;
+    }
+    void release()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct HostState {
+    hipStream_t stream = nullptr;
+    DevBuf in, out, counts, entries, ids, ctx;
+    void release()
+    {
+        in.release();
+        out.release();
+        counts.release();
+        entries.release();
+        ids.release();
+        ctx.release();
+        if (stream)
+            (void)hipStreamDestroy(stream);
+        stream = nullptr;
+    }
+};
+
+}  // namespace qi
+
+struct qi_plan {
+    int k = 0, m = 0, sys = 0, code_len = 0, n_outputs = 0, n = 0, K = 0;
+    uint32_t r = 0;
+    int device = 0;
+    int32_t* d_twist = nullptr;  // encode twist factors (non-systematic)
+    int32_t* d_gen = nullptr;    // generator matrix block (matrix encode)
+    qi::MatLayout gen{0, 0, 0};
+    uint32_t* d_err = nullptr;
+    qi::HostState host;
+};

@@ -1,0 +1,255 @@
+"""GPU parity: the HIP path (through the C-ABIs) against the reference's
+golden vectors and the CPU oracle, bit-exact.  Run with -m gpu."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from qi_testlib import (Q, codec, golden_names, load, oracle,
+                        oracle_decode_blocks, oracle_encode_blocks)
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+# --------------------------------------------------------------- helpers
+
+def fec_encode(hip_lib, k, m, sys_, data, cap):
+    import quadiron_amd as qa
+    f = qa.Fec(k, m, sys_)
+    no = f.n_outputs
+    B = data.shape[1]
+    outs = np.zeros((no, B), np.uint8)
+    oor = np.zeros((no, cap), np.uint32)
+    cnt = np.zeros(no, np.uint32)
+    rows = [np.ascontiguousarray(data[i]) for i in range(k)]
+    rc = hip_lib.qi_fec_encode_blocks(
+        f.h, qa.ptr_array(rows), qa.ptr_array([outs[i] for i in range(no)]),
+        B, oor.ctypes.data_as(C.c_void_p), cnt.ctypes.data_as(C.c_void_p),
+        cap)
+    assert rc == 0
+    return outs, oor, cnt
+
+
+def fec_decode(hip_lib, k, m, sys_, outputs, oor, cnt, missing, data):
+    import quadiron_amd as qa
+    f = qa.Fec(k, m, sys_)
+    B = outputs.shape[1]
+    dec = [np.zeros(B, np.uint8) if (not sys_ or missing[i]) else
+           data[i].copy() for i in range(k)]
+    par = [None if missing[(k + i) if sys_ else i] else outputs[i].copy()
+           for i in range(f.n_outputs)]
+    missing = np.ascontiguousarray(missing, np.int32)
+    wanted = np.ones(k, np.int32)
+    rc = hip_lib.qi_fec_decode_blocks(
+        f.h, qa.ptr_array(dec), qa.ptr_array(par),
+        oor.ctypes.data_as(C.c_void_p), cnt.ctypes.data_as(C.c_void_p),
+        oor.shape[1], missing.ctypes.data_as(C.c_void_p),
+        wanted.ctypes.data_as(C.c_void_p), B)
+    return rc, np.stack(dec)
+
+
+# ------------------------------------------------- golden (reference) tests
+
+@pytest.mark.parametrize("name", golden_names("blk_"))
+def test_blocks_vs_reference_golden(hip_lib, name):
+    g = load(name)
+    k, m, sys_, pkt, B, cap = (int(v) for v in g["params"])
+    outs, oor, cnt = fec_encode(hip_lib, k, m, sys_, g["data"], cap)
+    assert (outs == g["outputs"]).all()
+    assert (cnt == g["oor_count"]).all()
+    assert (oor == g["oor"]).all()
+    for p in range(len(g["missing"])):
+        rc, dec = fec_decode(hip_lib, k, m, sys_, g["outputs"], g["oor"],
+                             g["oor_count"], g["missing"][p], g["data"])
+        assert rc == 1
+        assert (dec == g["decoded"][p]).all()
+
+
+@pytest.mark.parametrize("name", golden_names("cabi_"))
+def test_cabi_vs_reference_golden(hip_lib, name):
+    import quadiron_amd as qa
+    g = load(name)
+    k, m, sys_, B, md = (int(v) for v in g["params"])
+    h = qa.QuadironFnt32(2, k, m, sys_)
+    assert h.metadata_size(B) == md
+    d = [g["data"][i].copy() for i in range(k)]
+    p = [np.zeros(md + B, np.uint8) for _ in range(m)]
+    wanted = np.ones(m if sys_ else k + m, np.int32)
+    assert h.encode(d, p, wanted, B) == 0
+    assert (np.stack(d) == g["enc_data"]).all()
+    assert (np.stack(p) == g["enc_parity"]).all()
+    for t in range(len(g["missing"])):
+        miss = np.ascontiguousarray(g["missing"][t], np.int32)
+        D = [g["enc_data"][i].copy() if not miss[i]
+             else np.zeros(md + B, np.uint8) for i in range(k)]
+        P = [g["enc_parity"][i].copy() if not miss[k + i]
+             else np.zeros(md + B, np.uint8) for i in range(m)]
+        assert h.decode(D, P, miss, B) == 0
+        assert (np.stack(D) == g["decoded"][t]).all()
+        D = [g["enc_data"][i].copy() if not miss[i]
+             else np.zeros(md + B, np.uint8) for i in range(k)]
+        P = [g["enc_parity"][i].copy() if not miss[k + i]
+             else np.zeros(md + B, np.uint8) for i in range(m)]
+        dest = int(g["dest"][t])
+        assert h.reconstruct(D, P, miss, dest, B) == 0
+        assert ((D + P)[dest] == g["reconstructed"][t]).all()
+
+
+def test_cabi_word_size_1_rejected(hip_lib):
+    import quadiron_amd as qa
+    assert hip_lib.quadiron_fnt32_new(1, 3, 3, 0) is None
+    with pytest.raises(ValueError):
+        qa.QuadironFnt32(1, 3, 3, 0)
+
+
+def test_cabi_errors(hip_lib):
+    import quadiron_amd as qa
+    k, m, B = 4, 2, 4096
+    h = qa.QuadironFnt32(2, k, m, 0)
+    md = h.metadata_size(B)
+    rng = np.random.default_rng(5)
+    d = [np.concatenate([np.zeros(md, np.uint8),
+                         rng.integers(0, 256, B, dtype=np.uint8)])
+         for _ in range(k)]
+    p = [np.zeros(md + B, np.uint8) for _ in range(m)]
+    assert h.encode(d, p, np.ones(k + m, np.int32), B) == 0
+    # fewer than k fragments
+    miss = np.zeros(k + m, np.int32)
+    miss[:m + 1] = 1
+    assert h.decode([x.copy() for x in d], [x.copy() for x in p], miss, B) == -1
+    # corrupt FNT1 magic of a present fragment
+    miss = np.zeros(k + m, np.int32)
+    miss[0] = 1
+    bad = [x.copy() for x in p]
+    bad[0][0] ^= 0xFF
+    assert h.decode([x.copy() for x in d], bad, miss, B) == -1
+
+
+# ------------------------------------------- device batch API vs oracle
+
+def _craft(k, m, sys_, data_rows, rng, n_cols):
+    """Force some outputs to 65536 (OOR) by solving for data row 0."""
+    o = oracle()
+    c = codec(k, m, sys_)
+    first = k if sys_ else 0
+    cw = (C.c_uint32 * c.n)()
+    din = (C.c_uint32 * k)()
+    ctx = C.create_string_buffer(40000)
+    if sys_:
+        o.qo_ctx_init(C.byref(c), ctx, (C.c_uint32 * k)(*range(k)))
+
+    def enc(vals):
+        for t in range(k):
+            din[t] = int(vals[t])
+        o.qo_encode_column(C.byref(c), ctx if sys_ else None, din, cw)
+        return [cw[first + i] for i in range(c.n_outputs)]
+
+    a = enc([1] + [0] * (k - 1))
+    P = data_rows.shape[1]
+    for j in rng.choice(P, min(n_cols, P), replace=False):
+        col = data_rows[:, j].astype(np.int64)
+        col[0] = 0
+        b = enc(col)
+        i = int(rng.integers(0, c.n_outputs))
+        if a[i] == 0:
+            continue
+        d0 = ((65536 - b[i]) % Q) * pow(a[i], Q - 2, Q) % Q
+        if d0 < 65536:
+            data_rows[0, j] = d0
+
+
+def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
+    torch = _torch()
+    import quadiron_amd as qa
+    rng = np.random.default_rng(seed)
+    plan = qa.Plan(k, m, sys_)
+    no = plan.n_outputs
+    data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
+    for s in range(min(S, 2)):
+        if n_craft:
+            _craft(k, m, sys_, data[s], rng, n_craft)
+    dd = torch.from_numpy(data.view(np.int16)).cuda()
+    out = torch.zeros((S, no, P), dtype=torch.int16, device="cuda")
+    cap = 64 + P // 512
+    counts = torch.zeros(S * no, dtype=torch.int32, device="cuda")
+    entries = torch.zeros(S * no * cap, dtype=torch.int32, device="cuda")
+    plan.encode(dd, out, counts, entries, cap)
+    torch.cuda.synchronize()
+    out_h = out.cpu().numpy().view(np.uint16)
+    cnt_h = counts.cpu().numpy().view(np.uint32).reshape(S, no)
+    ent_h = entries.cpu().numpy().view(np.uint32).reshape(S, no, cap)
+    assert (cnt_h <= cap).all()
+    if check_oracle:
+        for s in range(min(S, 3)):
+            bytes_rows = data[s].view(np.uint8).reshape(k, 2 * P)
+            o_out, o_oor, o_cnt = oracle_encode_blocks(k, m, sys_, bytes_rows,
+                                                       cap)
+            assert (out_h[s].view(np.uint8).reshape(no, 2 * P) == o_out).all()
+            assert (cnt_h[s] == o_cnt).all()
+            for i in range(no):
+                assert (np.sort(ent_h[s, i, :cnt_h[s, i]])
+                        == o_oor[i, :o_cnt[i]]).all()
+    # decode with a random k-subset per stripe (sys: drop a random data row
+    # set so that a real decode happens)
+    ids = np.zeros((S, k), np.uint16)
+    for s in range(S):
+        ids[s] = np.sort(rng.choice(k + m, k, replace=False))
+    di = torch.from_numpy(ids.view(np.int16)).cuda()
+    ctx = torch.zeros(plan.ctx_bytes(S), dtype=torch.uint8, device="cuda")
+    plan.decode_ctx(di, ctx, h_ids=ids)
+    dec = torch.zeros((S, k, P), dtype=torch.int16, device="cuda")
+    err = plan.decode(ctx, di, out, dec, data=dd, counts=counts,
+                      entries=entries, cap=cap)
+    torch.cuda.synchronize()
+    assert err == 0
+    assert (dec.cpu().numpy().view(np.uint16) == data).all()
+    return plan
+
+
+@pytest.mark.parametrize("k,m,sys_,S,P", [
+    (4, 4, 0, 100, 512),      # cfg1 shape
+    (16, 48, 0, 8, 4096),     # cfg2 shape, small P
+    (16, 48, 0, 3, 4093),     # ragged P (tail columns)
+    (16, 48, 1, 4, 2048),     # systematic
+    (3, 3, 0, 5, 1000),
+    (9, 5, 1, 5, 999),
+    (1, 1, 0, 2, 300),
+    (7, 1, 1, 2, 300),
+    (32, 32, 0, 2, 1024),
+    (33, 31, 0, 2, 513),      # K = 64 codelet, k not a power of two
+    (64, 960, 0, 2, 2048),    # cfg3 shape
+    (100, 28, 0, 1, 256),     # K = 128: matrix encode path, host ctx
+])
+def test_batch_vs_oracle(k, m, sys_, S, P):
+    _batch_roundtrip(k, m, sys_, S, P, seed=k * 1000 + m + P,
+                     n_craft=16 if k <= 64 else 0)
+
+
+def test_cfg2_full_size_roundtrip():
+    """BASELINE cfg2 geometry (k=16, n=64, 64 KiB packets) at 32 stripes:
+    encode -> per-stripe random erasures -> decode == data, and stripe 0
+    bit-exact against the oracle."""
+    _batch_roundtrip(16, 48, 0, 32, 32768, seed=2, n_craft=8,
+                     check_oracle=True)
+
+
+def test_cfg4_all_patterns_distinct():
+    """cfg4: per-stripe n-k random erasures (every stripe its own context)."""
+    _batch_roundtrip(16, 48, 0, 256, 2048, seed=4, n_craft=0,
+                     check_oracle=False)
+
+
+def test_empty_and_tiny_blocks(hip_lib):
+    for B in (0, 1, 2, 3, 130):
+        k, m = 3, 2
+        data = np.random.default_rng(B).integers(0, 256, (k, B),
+                                                 dtype=np.uint8)
+        outs, oor, cnt = fec_encode(hip_lib, k, m, 0, data, 64)
+        o_out, o_oor, o_cnt = oracle_encode_blocks(k, m, 0, data, 64)
+        assert (outs == o_out).all() and (cnt == o_cnt).all()
