@@ -26,25 +26,20 @@ __device__ __forceinline__ void record_oor(const Oor& o, int s, int slot,
             static_cast<uint32_t>(col);
 }
 
-// T-range value -> stored u16 (65536 and its alias -1 are stored as 0, the
-// truncation of vec::unpack src/vec_cast.h:133-163), recording the OOR mark
-// of src/fec_rs_fnt.h:253-269 when asked.
-__device__ __forceinline__ uint32_t emit(int32_t y, bool rec, const Oor& o,
-                                         int s, int slot, long long col)
+// T-range value -> stored u16: 65536 and its alias -1 are stored as 0 (the
+// truncation of vec::unpack src/vec_cast.h:133-163).
+__device__ __forceinline__ uint32_t fix16(int32_t y)
 {
-    if (static_cast<uint32_t>(y) > 65535u) {
-        if (rec)
-            record_oor(o, s, slot, col);
-        return 0u;
-    }
-    return static_cast<uint32_t>(y);
+    return static_cast<uint32_t>(y) > 65535u ? 0u : static_cast<uint32_t>(y);
 }
 
-template <int COLS>
-__device__ __forceinline__ void load_cols(const uint16_t* p, bool full,
-                                          long long avail, int32_t* v)
+// Loads of COLS adjacent u16 columns.  FULL: one dword / dwordx2 per lane;
+// otherwise the lane masks columns past `avail`.
+template <int COLS, bool FULL>
+__device__ __forceinline__ void load_cols(const uint16_t* p, long long avail,
+                                          int32_t* v)
 {
-    if (full) {
+    if constexpr (FULL) {
         if constexpr (COLS == 1) {
             v[0] = p[0];
         } else if constexpr (COLS == 2) {
@@ -65,19 +60,19 @@ __device__ __forceinline__ void load_cols(const uint16_t* p, bool full,
     }
 }
 
-template <int COLS>
-__device__ __forceinline__ void store_cols(uint16_t* p, bool full,
-                                           long long avail, const uint32_t* v)
+template <int COLS, bool FULL>
+__device__ __forceinline__ void store_cols(uint16_t* p, long long avail,
+                                           const uint32_t* v)
 {
-    if (full) {
+    if constexpr (FULL) {
         if constexpr (COLS == 1) {
             p[0] = static_cast<uint16_t>(v[0]);
         } else if constexpr (COLS == 2) {
-            *reinterpret_cast<uint32_t*>(p) = v[0] | (v[1] << 16);
+            *reinterpret_cast<uint32_t*>(p) = (v[0] & 0xffff) | (v[1] << 16);
         } else {
             uint2 w;
-            w.x = v[0] | (v[1] << 16);
-            w.y = v[2] | (v[3] << 16);
+            w.x = (v[0] & 0xffff) | (v[1] << 16);
+            w.y = (v[2] & 0xffff) | (v[3] << 16);
             *reinterpret_cast<uint2*>(p) = w;
         }
     } else {
@@ -96,8 +91,80 @@ __device__ __forceinline__ void store_cols(uint16_t* p, bool full,
 // into n/K twisted K-point transforms:
 //     out[(n/K) u + v] = sum_{t<K} (d_t w^{vt}) wK^{ut}
 // so a lane keeps only 2K values per column live, and pass v writes the K
-// output rows {(n/K)u + v}.
+// output rows {(n/K)u + v}.  All loads of a lane are issued back to back
+// (branch-free), outputs are stored as soon as a pass is done, and the rare
+// out-of-range outputs (value 65536, src/fec_rs_fnt.h:253-269) are found by
+// one OR-reduction per pass and fixed up off the fast path.
 // ---------------------------------------------------------------------------
+template <int K, int COLS, bool FULL>
+__device__ __forceinline__ void encode_body(
+    int k, int n, int n_out, const int32_t* __restrict__ twist,
+    const uint16_t* __restrict__ src, long long drs, uint16_t* __restrict__ dst,
+    long long ors, long long col, long long avail, int s, const Oor& oor)
+{
+    const bool rec = oor.counts != nullptr;
+    int32_t x[COLS][K];
+#pragma unroll
+    for (int t = 0; t < K; t++) {
+        const int row = t < k ? t : k - 1;  // branch-free: clamp, then mask
+        int32_t v[COLS];
+        load_cols<COLS, FULL>(src + row * drs, avail, v);
+#pragma unroll
+        for (int c = 0; c < COLS; c++)
+            x[c][t] = t < k ? v[c] : 0;
+    }
+
+    const int passes = n / K;
+    for (int v = 0; v < passes; v++) {
+        int32_t y[COLS][K];
+        const int32_t* tw = twist + v * K;
+#pragma unroll
+        for (int t = 0; t < K; t++) {
+            const int32_t cb = tw[t];
+#pragma unroll
+            for (int c = 0; c < COLS; c++)
+                y[c][t] = t == 0 ? x[c][t] : mul_data(x[c][t], cb);
+        }
+#pragma unroll
+        for (int c = 0; c < COLS; c++)
+            dft<K>(y[c]);
+        uint32_t bad = 0;
+#pragma unroll
+        for (int u = 0; u < K; u++) {
+            const int row = passes * u + v;
+            uint32_t o[COLS];
+#pragma unroll
+            for (int c = 0; c < COLS; c++) {
+                y[c][u] = fold(y[c][u]);  // T-range
+                o[c] = static_cast<uint32_t>(y[c][u]);
+                bad |= o[c];
+            }
+            if (row < n_out)
+                store_cols<COLS, FULL>(dst + row * ors, avail, o);
+        }
+        if (__builtin_expect((bad >> 16) != 0, 0)) {
+            // rare: some output of this pass is 65536 (stored as 0 + mark)
+#pragma unroll
+            for (int u = 0; u < K; u++) {
+                const int row = passes * u + v;
+                bool any = false;
+                uint32_t o[COLS];
+#pragma unroll
+                for (int c = 0; c < COLS; c++) {
+                    o[c] = fix16(y[c][u]);
+                    if (static_cast<uint32_t>(y[c][u]) > 65535u && row < n_out) {
+                        any = true;
+                        if (rec && c < avail)
+                            record_oor(oor, s, row, col + c);
+                    }
+                }
+                if (any)
+                    store_cols<COLS, FULL>(dst + row * ors, avail, o);
+            }
+        }
+    }
+}
+
 template <int K, int COLS>
 __global__ __launch_bounds__(kBlock) void encode_fnt_kernel(
     int k, int n, int n_out, const int32_t* __restrict__ twist,
@@ -108,65 +175,18 @@ __global__ __launch_bounds__(kBlock) void encode_fnt_kernel(
     const int b = blockIdx.x;
     const int s = b / tiles;
     const int tile = b - s * tiles;
-    const long long col =
-        (static_cast<long long>(tile) * kBlock + threadIdx.x) * COLS;
-    if (col >= words)
-        return;
-    const long long avail = words - col;
-    const bool full = avail >= COLS;
-    const bool rec = oor.counts != nullptr;
-
-    int32_t x[COLS][K];
+    const long long col0 = static_cast<long long>(tile) * kBlock * COLS;
+    const long long col = col0 + static_cast<long long>(threadIdx.x) * COLS;
     const uint16_t* src = data + s * dss + col;
-#pragma unroll
-    for (int t = 0; t < K; t++) {
-        int32_t v[COLS];
-        if (t < k) {
-            load_cols<COLS>(src + t * drs, full, avail, v);
-        } else {
-#pragma unroll
-            for (int c = 0; c < COLS; c++)
-                v[c] = 0;
-        }
-#pragma unroll
-        for (int c = 0; c < COLS; c++)
-            x[c][t] = v[c];
-    }
-
-    const int passes = n / K;
     uint16_t* dst = out + s * oss + col;
-    for (int v = 0; v < passes; v++) {
-        int32_t y[COLS][K];
-        if (v == 0) {
-#pragma unroll
-            for (int c = 0; c < COLS; c++)
-#pragma unroll
-                for (int t = 0; t < K; t++)
-                    y[c][t] = x[c][t];
-        } else {
-            const int32_t* tw = twist + v * K;
-#pragma unroll
-            for (int t = 0; t < K; t++) {
-                const int32_t cb = tw[t];
-#pragma unroll
-                for (int c = 0; c < COLS; c++)
-                    y[c][t] = t == 0 ? x[c][t] : mul_data(x[c][t], cb);
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < COLS; c++)
-            dft<K>(y[c]);
-#pragma unroll
-        for (int u = 0; u < K; u++) {
-            const int row = passes * u + v;
-            if (row < n_out) {
-                uint32_t o[COLS];
-#pragma unroll
-                for (int c = 0; c < COLS; c++)
-                    o[c] = emit(fold(y[c][u]), rec, oor, s, row, col + c);
-                store_cols<COLS>(dst + row * ors, full, avail, o);
-            }
-        }
+    if (col0 + kBlock * COLS <= words) {  // block-uniform
+        encode_body<K, COLS, true>(k, n, n_out, twist, src, drs, dst, ors, col,
+                                   COLS, s, oor);
+    } else {
+        if (col >= words)
+            return;
+        encode_body<K, COLS, false>(k, n, n_out, twist, src, drs, dst, ors,
+                                    col, words - col, s, oor);
     }
 }
 
@@ -178,6 +198,100 @@ __global__ __launch_bounds__(kBlock) void encode_fnt_kernel(
 // as one k x k product), systematic decode and systematic encode.
 // ---------------------------------------------------------------------------
 constexpr int kMaxTileOor = 256;
+typedef short qi_short2 __attribute__((ext_vector_type(2)));
+
+template <int KP, int COLS, bool FULL>
+__device__ __forceinline__ void matrix_body(
+    const MatLayout& L, const int32_t* __restrict__ M, const uint16_t* sid,
+    const RowSrc& src, uint16_t* __restrict__ obase, long long ors,
+    long long col, long long avail, int s, int n_marks, const int* s_i,
+    const uint32_t* s_col, const Oor& out_oor)
+{
+    const int kin = L.kin;
+    // load every received row (branch-free; rows past kin are masked to 0)
+    int32_t xp[COLS][KP];
+#pragma unroll
+    for (int j = 0; j < KP; j++) {
+        int32_t vv[2][COLS];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int i = 2 * j + h;
+            const int ii = i < kin ? i : kin - 1;
+            const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
+            const uint16_t* p =
+                id < src.split ? src.base0 + s * src.ss0 + id * src.rs0
+                               : src.base1 + s * src.ss1 + (id - src.split) * src.rs1;
+            load_cols<COLS, FULL>(p + col, avail, vv[h]);
+#pragma unroll
+            for (int c = 0; c < COLS; c++)
+                vv[h][c] = i < kin ? vv[h][c] : 0;
+        }
+        // offset to signed 16 bit (x - 32768) and pack the row pair
+#pragma unroll
+        for (int c = 0; c < COLS; c++)
+            xp[c][j] = static_cast<int32_t>(
+                (static_cast<uint32_t>(vv[0][c]) |
+                 (static_cast<uint32_t>(vv[1][c]) << 16)) ^
+                0x80008000u);
+    }
+
+    const int32_t* kcorr = M + L.kcorr();
+    const int32_t* rscale = M + L.rscale();
+    const int32_t* plain = M + L.plain();
+    const bool rec = out_oor.counts != nullptr;
+    for (int t = 0; t < L.R; t++) {
+        const int32_t* mrow = M + t * KP;
+        int32_t acc[COLS];
+#pragma unroll
+        for (int c = 0; c < COLS; c++)
+            acc[c] = kcorr[t];
+#pragma unroll
+        for (int j = 0; j < KP; j++) {
+            const qi_short2 m2 = __builtin_bit_cast(qi_short2, mrow[j]);
+#pragma unroll
+            for (int c = 0; c < COLS; c++)
+                acc[c] = fold(__builtin_amdgcn_sdot2(
+                    __builtin_bit_cast(qi_short2, xp[c][j]), m2, acc[c], false));
+        }
+        int32_t y[COLS];
+#pragma unroll
+        for (int c = 0; c < COLS; c++)
+            y[c] = fold(acc[c]);  // T-range
+        for (int e = 0; e < n_marks; e++) {
+            // restored symbol is 65536 == -1 where the stored word is 0
+            const long long d = static_cast<long long>(s_col[e]) - col;
+            if (d >= 0 && d < COLS) {
+                const int32_t corr = plain[t * kin + s_i[e]];
+#pragma unroll
+                for (int c = 0; c < COLS; c++)
+                    if (c == d)
+                        y[c] = fold(fold(y[c] - corr));
+            }
+        }
+        const int32_t rs = rscale[t];
+        if (rs != 1) {
+#pragma unroll
+            for (int c = 0; c < COLS; c++)
+                y[c] = fold(fold(y[c] * rs));
+        }
+        uint32_t o[COLS];
+        uint32_t bad = 0;
+#pragma unroll
+        for (int c = 0; c < COLS; c++) {
+            o[c] = static_cast<uint32_t>(y[c]);
+            bad |= o[c];
+        }
+        if (__builtin_expect((bad >> 16) != 0, 0)) {
+#pragma unroll
+            for (int c = 0; c < COLS; c++) {
+                if (static_cast<uint32_t>(y[c]) > 65535u && rec && c < avail)
+                    record_oor(out_oor, s, t, col + c);
+                o[c] = fix16(y[c]);
+            }
+        }
+        store_cols<COLS, FULL>(obase + t * ors, avail, o);
+    }
+}
 
 template <int KP, int COLS>
 __global__ __launch_bounds__(kBlock) void matrix_kernel(
@@ -194,8 +308,7 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
     const int tile = b - s * tiles;
     const int kin = L.kin;
     const long long col0 = static_cast<long long>(tile) * kBlock * COLS;
-    const long long col =
-        col0 + static_cast<long long>(threadIdx.x) * COLS;
+    const long long col = col0 + static_cast<long long>(threadIdx.x) * COLS;
     const int32_t* M = mat + s * mat_stride;
     const uint16_t* sid = ids ? ids + static_cast<long long>(s) * kin : nullptr;
 
@@ -232,87 +345,16 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
         __syncthreads();
         n_marks = min(s_cnt, kMaxTileOor);
     }
-    if (col >= words)
-        return;
-    const long long avail = words - col;
-    const bool full = avail >= COLS;
-
-    // load received rows, offset to signed 16-bit and pack row pairs
-    int32_t xp[COLS][KP];
-#pragma unroll
-    for (int j = 0; j < KP; j++) {
-        int32_t v0[COLS], v1[COLS];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int i = 2 * j + h;
-            int32_t* v = h ? v1 : v0;
-            if (i < kin) {
-                const int id = src.by_pos ? i : (sid ? sid[i] : i);
-                const uint16_t* p =
-                    id < src.split
-                        ? src.base0 + s * src.ss0 + id * src.rs0
-                        : src.base1 + s * src.ss1 + (id - src.split) * src.rs1;
-                load_cols<COLS>(p + col, full, avail, v);
-            } else {
-#pragma unroll
-                for (int c = 0; c < COLS; c++)
-                    v[c] = 0;
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < COLS; c++)
-            xp[c][j] = static_cast<int32_t>(
-                ((static_cast<uint32_t>(v0[c]) | (static_cast<uint32_t>(v1[c]) << 16))) ^
-                0x80008000u);
-    }
-
-    const int32_t* kcorr = M + L.kcorr();
-    const int32_t* rscale = M + L.rscale();
-    const int32_t* plain = M + L.plain();
-    const bool rec = out_oor.counts != nullptr;
     uint16_t* obase = dst.base + s * dst.ss + col;
-    typedef short short2_t __attribute__((ext_vector_type(2)));
-
-    for (int t = 0; t < L.R; t++) {
-        const int32_t* mrow = M + t * KP;
-        int32_t acc[COLS];
-#pragma unroll
-        for (int c = 0; c < COLS; c++)
-            acc[c] = kcorr[t];
-#pragma unroll
-        for (int j = 0; j < KP; j++) {
-            const short2_t m2 = __builtin_bit_cast(short2_t, mrow[j]);
-#pragma unroll
-            for (int c = 0; c < COLS; c++)
-                acc[c] = fold(__builtin_amdgcn_sdot2(
-                    __builtin_bit_cast(short2_t, xp[c][j]), m2, acc[c], false));
-        }
-        int32_t y[COLS];
-#pragma unroll
-        for (int c = 0; c < COLS; c++)
-            y[c] = fold(acc[c]);  // T-range
-        for (int e = 0; e < n_marks; e++) {
-            // restored symbol is 65536 == -1 where the stored word is 0
-            const long long d = static_cast<long long>(s_col[e]) - col;
-            if (d >= 0 && d < COLS) {
-                const int32_t corr = plain[t * kin + s_i[e]];
-#pragma unroll
-                for (int c = 0; c < COLS; c++)
-                    if (c == d)
-                        y[c] = fold(fold(y[c] - corr));
-            }
-        }
-        const int32_t rs = rscale[t];
-        if (rs != 1) {
-#pragma unroll
-            for (int c = 0; c < COLS; c++)
-                y[c] = fold(fold(y[c] * rs));
-        }
-        uint32_t o[COLS];
-#pragma unroll
-        for (int c = 0; c < COLS; c++)
-            o[c] = emit(y[c], rec, out_oor, s, t, col + c);
-        store_cols<COLS>(obase + t * dst.rs, full, avail, o);
+    if (col0 + kBlock * COLS <= words) {  // block-uniform
+        matrix_body<KP, COLS, true>(L, M, sid, src, obase, dst.rs, col, COLS, s,
+                                    n_marks, s_i, s_col, out_oor);
+    } else {
+        if (col >= words)
+            return;
+        matrix_body<KP, COLS, false>(L, M, sid, src, obase, dst.rs, col,
+                                     words - col, s, n_marks, s_i, s_col,
+                                     out_oor);
     }
 }
 
