@@ -26,6 +26,14 @@
 #define QI_HD inline
 #endif
 
+#if defined(QI_HOST_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
+#include <cassert>
+// host test builds: v_mul_i32_i24 operands must fit 24 bits
+#define QI_ASSERT24(x) assert((x) > -(1 << 23) && (x) < (1 << 23))
+#else
+#define QI_ASSERT24(x) ((void)0)
+#endif
+
 namespace qi {
 
 constexpr int32_t kQ = 65537;
@@ -109,6 +117,7 @@ template <uint32_t C>
 QI_HD int32_t mul_tw(int32_t x)
 {
     constexpr int32_t cb = balanced(C);
+    QI_ASSERT24(x);
     if constexpr (C == 1u) {
         return x;
     } else if constexpr (cb == 32768 || cb == -32768) {

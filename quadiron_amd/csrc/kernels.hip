@@ -33,6 +33,20 @@ __device__ __forceinline__ uint32_t fix16(int32_t y)
     return static_cast<uint32_t>(y) > 65535u ? 0u : static_cast<uint32_t>(y);
 }
 
+// canonical residue of a V-range value [-2, 65537]
+__device__ __forceinline__ uint32_t canon_v(int32_t y)
+{
+    const int32_t c = y < 0 ? y + 65537 : y;
+    return static_cast<uint32_t>(c >= 65537 ? c - 65537 : c);
+}
+
+constexpr long long kTwLo = -32767, kTwHi = 98303;
+static_assert(fold_rng(join(mul_rng(Rng{0, 65535}, 32768),
+                            mul_rng(Rng{0, 65535}, -32768))).lo == kTwLo &&
+                  fold_rng(join(mul_rng(Rng{0, 65535}, 32768),
+                                mul_rng(Rng{0, 65535}, -32768))).hi == kTwHi,
+              "twist output range");
+
 // Loads of COLS adjacent u16 columns.  FULL: one dword / dwordx2 per lane;
 // otherwise the lane masks columns past `avail`.
 template <int COLS, bool FULL>
@@ -117,17 +131,33 @@ __device__ __forceinline__ void encode_body(
     const int passes = n / K;
     for (int v = 0; v < passes; v++) {
         int32_t y[COLS][K];
-        const int32_t* tw = twist + v * K;
+        if (v == 0) {
 #pragma unroll
-        for (int t = 0; t < K; t++) {
-            const int32_t cb = tw[t];
+            for (int c = 0; c < COLS; c++) {
+#pragma unroll
+                for (int t = 0; t < K; t++)
+                    y[c][t] = x[c][t];
+                dft<K, 0, 65535>(y[c]);
+            }
+        } else {
+            // twist by w^{vt}: |x*c| < 2^31 for x < 2^16, |c| <= 2^15, and
+            // one fold leaves [-32767, 98303] (kTwLo/kTwHi), which the
+            // codelet plan accepts as its input range
+            const int32_t* tw = twist + v * K;
+#pragma unroll
+            for (int t = 0; t < K; t++) {
+                const int32_t cb = tw[t];
+#pragma unroll
+                for (int c = 0; c < COLS; c++)
+                    y[c][t] = t == 0 ? x[c][t] : fold(x[c][t] * cb);
+            }
 #pragma unroll
             for (int c = 0; c < COLS; c++)
-                y[c][t] = t == 0 ? x[c][t] : mul_data(x[c][t], cb);
+                dft<K, kTwLo, kTwHi>(y[c]);
         }
-#pragma unroll
-        for (int c = 0; c < COLS; c++)
-            dft<K>(y[c]);
+        // outputs are in V = [-2, 65537]: the fast path stores the low 16
+        // bits; any value outside [0, 65535] (the true OOR symbol 65536 or a
+        // non-canonical alias) sends the pass through the fix-up below
         uint32_t bad = 0;
 #pragma unroll
         for (int u = 0; u < K; u++) {
@@ -135,7 +165,6 @@ __device__ __forceinline__ void encode_body(
             uint32_t o[COLS];
 #pragma unroll
             for (int c = 0; c < COLS; c++) {
-                y[c][u] = fold(y[c][u]);  // T-range
                 o[c] = static_cast<uint32_t>(y[c][u]);
                 bad |= o[c];
             }
@@ -143,7 +172,6 @@ __device__ __forceinline__ void encode_body(
                 store_cols<COLS, FULL>(dst + row * ors, avail, o);
         }
         if (__builtin_expect((bad >> 16) != 0, 0)) {
-            // rare: some output of this pass is 65536 (stored as 0 + mark)
 #pragma unroll
             for (int u = 0; u < K; u++) {
                 const int row = passes * u + v;
@@ -151,10 +179,11 @@ __device__ __forceinline__ void encode_body(
                 uint32_t o[COLS];
 #pragma unroll
                 for (int c = 0; c < COLS; c++) {
-                    o[c] = fix16(y[c][u]);
+                    const uint32_t cv = canon_v(y[c][u]);
+                    o[c] = cv & 0xffffu;
                     if (static_cast<uint32_t>(y[c][u]) > 65535u && row < n_out) {
                         any = true;
-                        if (rec && c < avail)
+                        if (rec && cv == 65536u && c < avail)
                             record_oor(oor, s, row, col + c);
                     }
                 }
@@ -201,15 +230,13 @@ constexpr int kMaxTileOor = 256;
 typedef short qi_short2 __attribute__((ext_vector_type(2)));
 
 template <int KP, int COLS, bool FULL>
-__device__ __forceinline__ void matrix_body(
-    const MatLayout& L, const int32_t* __restrict__ M, const uint16_t* sid,
-    const RowSrc& src, uint16_t* __restrict__ obase, long long ors,
-    long long col, long long avail, int s, int n_marks, const int* s_i,
-    const uint32_t* s_col, const Oor& out_oor)
+__device__ __forceinline__ void matrix_load(int kin, const uint16_t* sid,
+                                            const RowSrc& src, long long col,
+                                            long long avail, int s,
+                                            int32_t (&xp)[COLS][KP])
 {
-    const int kin = L.kin;
-    // load every received row (branch-free; rows past kin are masked to 0)
-    int32_t xp[COLS][KP];
+    // every received row, branch-free (rows past kin are masked to 0), then
+    // offset to signed 16 bit (x - 32768) and pack row pairs for dot2
 #pragma unroll
     for (int j = 0; j < KP; j++) {
         int32_t vv[2][COLS];
@@ -226,7 +253,6 @@ __device__ __forceinline__ void matrix_body(
             for (int c = 0; c < COLS; c++)
                 vv[h][c] = i < kin ? vv[h][c] : 0;
         }
-        // offset to signed 16 bit (x - 32768) and pack the row pair
 #pragma unroll
         for (int c = 0; c < COLS; c++)
             xp[c][j] = static_cast<int32_t>(
@@ -234,13 +260,22 @@ __device__ __forceinline__ void matrix_body(
                  (static_cast<uint32_t>(vv[1][c]) << 16)) ^
                 0x80008000u);
     }
+}
 
-    const int32_t* kcorr = M + L.kcorr();
-    const int32_t* rscale = M + L.rscale();
-    const int32_t* plain = M + L.plain();
+template <int KP, int COLS, bool FULL>
+__device__ __forceinline__ void matrix_compute(
+    const MatLayout& L, const int32_t* sm, const int32_t* __restrict__ plain,
+    const int32_t (&xp)[COLS][KP], uint16_t* __restrict__ obase, long long ors,
+    long long col, long long avail, int s, int n_marks, const int* s_i,
+    const uint32_t* s_col, const Oor& out_oor)
+{
+    // sm: the packed matrix, kcorr and rscale staged in LDS
+    const int kin = L.kin;
+    const int32_t* kcorr = sm + L.kcorr();
+    const int32_t* rscale = sm + L.rscale();
     const bool rec = out_oor.counts != nullptr;
     for (int t = 0; t < L.R; t++) {
-        const int32_t* mrow = M + t * KP;
+        const int32_t* mrow = sm + t * KP;
         int32_t acc[COLS];
 #pragma unroll
         for (int c = 0; c < COLS; c++)
@@ -299,6 +334,7 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
     const uint16_t* __restrict__ ids, RowSrc src, RowDst dst, long long words,
     int tiles, Oor in_oor, int slot_base, Oor out_oor, uint32_t* err)
 {
+    extern __shared__ int32_t s_mat[];  // packed + kcorr + rscale
     __shared__ int s_cnt;
     __shared__ int s_i[kMaxTileOor];
     __shared__ uint32_t s_col[kMaxTileOor];
@@ -311,14 +347,25 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
     const long long col = col0 + static_cast<long long>(threadIdx.x) * COLS;
     const int32_t* M = mat + s * mat_stride;
     const uint16_t* sid = ids ? ids + static_cast<long long>(s) * kin : nullptr;
+    const bool full = col0 + kBlock * COLS <= words;  // block-uniform
 
-    // gather this tile's OOR marks of the received rows
-    // (decode_prepare, src/fec_base.h:1361-1404)
+    // 1) issue every row load of this lane first
+    int32_t xp[COLS][KP];
+    if (full) {
+        matrix_load<KP, COLS, true>(kin, sid, src, col, COLS, s, xp);
+    } else if (col < words) {
+        matrix_load<KP, COLS, false>(kin, sid, src, col, words - col, s, xp);
+    }
+    // 2) meanwhile stage the matrix rows in LDS and gather this tile's OOR
+    //    marks of the received rows (decode_prepare, src/fec_base.h:1361-1404)
+    const int nm = static_cast<int>(L.plain());
+    for (int i = threadIdx.x; i < nm; i += kBlock)
+        s_mat[i] = M[i];
+    if (threadIdx.x == 0)
+        s_cnt = 0;
+    __syncthreads();
     int n_marks = 0;
     if (in_oor.counts) {
-        if (threadIdx.x == 0)
-            s_cnt = 0;
-        __syncthreads();
         const long long col1 = col0 + kBlock * COLS;
         for (int i = threadIdx.x; i < kin; i += kBlock) {
             const int id = sid ? sid[i] : i;
@@ -342,19 +389,18 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
                 }
             }
         }
-        __syncthreads();
-        n_marks = min(s_cnt, kMaxTileOor);
     }
+    __syncthreads();
+    n_marks = min(s_cnt, kMaxTileOor);
     uint16_t* obase = dst.base + s * dst.ss + col;
-    if (col0 + kBlock * COLS <= words) {  // block-uniform
-        matrix_body<KP, COLS, true>(L, M, sid, src, obase, dst.rs, col, COLS, s,
-                                    n_marks, s_i, s_col, out_oor);
-    } else {
-        if (col >= words)
-            return;
-        matrix_body<KP, COLS, false>(L, M, sid, src, obase, dst.rs, col,
-                                     words - col, s, n_marks, s_i, s_col,
-                                     out_oor);
+    const int32_t* plain = M + L.plain();
+    if (full) {
+        matrix_compute<KP, COLS, true>(L, s_mat, plain, xp, obase, dst.rs, col,
+                                       COLS, s, n_marks, s_i, s_col, out_oor);
+    } else if (col < words) {
+        matrix_compute<KP, COLS, false>(L, s_mat, plain, xp, obase, dst.rs, col,
+                                        words - col, s, n_marks, s_i, s_col,
+                                        out_oor);
     }
 }
 
@@ -523,8 +569,11 @@ static int mat_launch(const MatLayout& L, const int32_t* mat, long long ms,
     int tiles;
     if (grid_for(words, COLS, S, &tiles))
         return -1;
+    const size_t lds = L.plain() * sizeof(int32_t);
+    if (lds > 64 * 1024)
+        return -5;
     hipLaunchKernelGGL((matrix_kernel<KP, COLS>), dim3(tiles * S), dim3(kBlock),
-                       0, st, L, mat, ms, ids, src, dst, words, tiles, in_oor,
+                       lds, st, L, mat, ms, ids, src, dst, words, tiles, in_oor,
                        slot_base, out_oor, err);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
