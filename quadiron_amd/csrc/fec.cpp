@@ -274,7 +274,7 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
              "qi_gpu_decode_ctx");
     // received rows staged by position; OOR buckets by position
     const MatLayout L{k, k, matrix_kp(k)};
-    RowSrc src{din, 0, static_cast<long long>(P), 1 << 30, nullptr, 0, 0, 1};
+    RowSrc src{din, 0, static_cast<long long>(P), 1 << 30, nullptr, 0, 0, 1, k, 0};
     RowDst dst{dout, 0, static_cast<long long>(P)};
     Oor in{reinterpret_cast<uint32_t*>(dcb + cnt_off),
            reinterpret_cast<uint32_t*>(dcb + ent_off), k,

@@ -110,6 +110,37 @@ constexpr uint32_t bitrev_c(uint32_t i, int bits)
     return r;
 }
 
+// 24-bit sign-extension: tells the compiler a value fits v_mul_i32_i24
+QI_HD int32_t sext24(int32_t c)
+{
+    return static_cast<int32_t>(static_cast<uint32_t>(c) << 8) >> 8;
+}
+
+// x * cb for a compile-time constant as ONE v_mul_i32_i24 with the constant
+// in an SGPR.  The constant is passed through an opaque s_mov so the
+// compiler cannot strength-reduce a power-of-two twiddle into shift/and/ashr
+// sequences, which would also defeat the single SDWA v_sub of the following
+// fold (4 VALU instead of 2).  The s_mov is CSE'd/hoisted (SALU, no VALU).
+template <int32_t CB>
+QI_HD int32_t mul_const(int32_t x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    int32_t c;
+    asm("s_mov_b32 %0, %1" : "=s"(c) : "i"(CB));
+    return x * sext24(c);
+#else
+    return x * CB;
+#endif
+}
+
+// x * c for a wave-uniform runtime constant c; the caller guarantees |x|,
+// |c| < 2^23 and |x*c| < 2^31 (the sign-extension lets the compiler use
+// v_mul_i32_i24 instead of the quarter-rate v_mul_lo_u32).
+QI_HD int32_t mul_i24_s(int32_t x, int32_t c)
+{
+    return x * sext24(c);
+}
+
 // x * c for a compile-time canonical twiddle c, x in V = [-2, 65537].
 // Result congruent to x*c, range [-32767, 98303] (or T-range pieces for the
 // trivial cases).
@@ -123,9 +154,9 @@ QI_HD int32_t mul_tw(int32_t x)
     } else if constexpr (cb == 32768 || cb == -32768) {
         // |x * 2^15| may reach 2^31: multiply by half, fold, double.
         // 2*fold(x*cb/2) in [-65534, 196606] -> fold again -> V.
-        return fold(2 * fold(x * (cb / 2)));
+        return fold(2 * fold(mul_const<cb / 2>(x)));
     } else {
-        return fold(x * cb);
+        return fold(mul_const<cb>(x));
     }
 }
 

@@ -6,6 +6,12 @@
 // contiguous 64*COLS*2-byte segment of one row (coalesced), and every column
 // -- an independent RS codeword read "vertically" across the fragments
 // (src/fec_base.h:1103-1150) -- is transformed entirely in VGPRs.
+//
+// Addressing: a stripe's rows are reached through a buffer resource (SGPR
+// base + 32-bit extent) with the row offset in an SGPR (soffset) and the
+// column offset in one VGPR (voffset), so no per-lane 64-bit address math is
+// spent per load/store.  Stripes whose extent does not fit 32 bits use the
+// BUF=false instantiation (flat global addressing).
 #include <hip/hip_runtime.h>
 
 #include "fnt_codelets.h"
@@ -20,7 +26,8 @@ constexpr int kBlock = 256;
 __device__ __forceinline__ void record_oor(const Oor& o, int s, int slot,
                                            long long col)
 {
-    const uint32_t e = atomicAdd(&o.counts[static_cast<long long>(s) * o.slots + slot], 1u);
+    const uint32_t e =
+        atomicAdd(&o.counts[static_cast<long long>(s) * o.slots + slot], 1u);
     if (e < static_cast<uint32_t>(o.cap))
         o.entries[(static_cast<long long>(s) * o.slots + slot) * o.cap + e] =
             static_cast<uint32_t>(col);
@@ -47,53 +54,85 @@ static_assert(fold_rng(join(mul_rng(Rng{0, 65535}, 32768),
                                 mul_rng(Rng{0, 65535}, -32768))).hi == kTwHi,
               "twist output range");
 
-// Loads of COLS adjacent u16 columns.  FULL: one dword / dwordx2 per lane;
-// otherwise the lane masks columns past `avail`.
-template <int COLS, bool FULL>
-__device__ __forceinline__ void load_cols(const uint16_t* p, long long avail,
-                                          int32_t* v)
+// pack the low halves of two dwords: [a.lo, b.lo] (one v_perm_b32)
+__device__ __forceinline__ uint32_t pack_lo(uint32_t a, uint32_t b)
 {
-    if constexpr (FULL) {
-        if constexpr (COLS == 1) {
-            v[0] = p[0];
-        } else if constexpr (COLS == 2) {
-            const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
-            v[0] = w & 0xffff;
-            v[1] = w >> 16;
-        } else {
-            const uint2 w = *reinterpret_cast<const uint2*>(p);
-            v[0] = w.x & 0xffff;
-            v[1] = w.x >> 16;
-            v[2] = w.y & 0xffff;
-            v[3] = w.y >> 16;
-        }
+    return __builtin_amdgcn_perm(b, a, 0x05040100u);
+}
+
+// A stripe region: buffer resource (BUF) or flat base pointer.
+template <bool BUF>
+struct Region {
+    __amdgpu_buffer_rsrc_t r;
+    char* p;
+    __device__ __forceinline__ Region(const void* base, uint32_t bytes)
+    {
+        p = static_cast<char*>(const_cast<void*>(base));
+        if constexpr (BUF)
+            r = __builtin_amdgcn_make_buffer_rsrc(p, static_cast<short>(0),
+                                                  static_cast<int>(bytes),
+                                                  0x00020000);
+    }
+};
+
+// COLS adjacent u16 columns of the row at byte offset `row` (wave-uniform).
+// FULL: one dword per lane (COLS 2); otherwise columns past `avail` are 0.
+template <int COLS, bool FULL, bool BUF>
+__device__ __forceinline__ void ld(const Region<BUF>& g, uint32_t row,
+                                   uint32_t voff, long long avail, int32_t* v)
+{
+    if constexpr (FULL && COLS == 2) {
+        uint32_t w;
+        if constexpr (BUF)
+            w = __builtin_amdgcn_raw_buffer_load_b32(g.r, static_cast<int>(voff),
+                                                     static_cast<int>(row), 0);
+        else
+            w = *reinterpret_cast<const uint32_t*>(g.p + row + voff);
+        v[0] = w & 0xffff;
+        v[1] = w >> 16;
     } else {
 #pragma unroll
-        for (int c = 0; c < COLS; c++)
-            v[c] = c < avail ? p[c] : 0;
+        for (int c = 0; c < COLS; c++) {
+            if (FULL || c < avail) {
+                if constexpr (BUF)
+                    v[c] = __builtin_amdgcn_raw_buffer_load_b16(
+                        g.r, static_cast<int>(voff + 2 * c),
+                        static_cast<int>(row), 0);
+                else
+                    v[c] = *reinterpret_cast<const uint16_t*>(g.p + row + voff +
+                                                              2 * c);
+            } else {
+                v[c] = 0;
+            }
+        }
     }
 }
 
-template <int COLS, bool FULL>
-__device__ __forceinline__ void store_cols(uint16_t* p, long long avail,
-                                           const uint32_t* v)
+template <int COLS, bool FULL, bool BUF>
+__device__ __forceinline__ void st(const Region<BUF>& g, uint32_t row,
+                                   uint32_t voff, long long avail,
+                                   const uint32_t* v)
 {
-    if constexpr (FULL) {
-        if constexpr (COLS == 1) {
-            p[0] = static_cast<uint16_t>(v[0]);
-        } else if constexpr (COLS == 2) {
-            *reinterpret_cast<uint32_t*>(p) = (v[0] & 0xffff) | (v[1] << 16);
-        } else {
-            uint2 w;
-            w.x = (v[0] & 0xffff) | (v[1] << 16);
-            w.y = (v[2] & 0xffff) | (v[3] << 16);
-            *reinterpret_cast<uint2*>(p) = w;
-        }
+    if constexpr (FULL && COLS == 2) {
+        const uint32_t w = pack_lo(v[0], v[1]);
+        if constexpr (BUF)
+            __builtin_amdgcn_raw_buffer_store_b32(w, g.r, static_cast<int>(voff),
+                                                  static_cast<int>(row), 0);
+        else
+            *reinterpret_cast<uint32_t*>(g.p + row + voff) = w;
     } else {
 #pragma unroll
-        for (int c = 0; c < COLS; c++)
-            if (c < avail)
-                p[c] = static_cast<uint16_t>(v[c]);
+        for (int c = 0; c < COLS; c++) {
+            if (FULL || c < avail) {
+                if constexpr (BUF)
+                    __builtin_amdgcn_raw_buffer_store_b16(
+                        static_cast<uint16_t>(v[c]), g.r,
+                        static_cast<int>(voff + 2 * c), static_cast<int>(row), 0);
+                else
+                    *reinterpret_cast<uint16_t*>(g.p + row + voff + 2 * c) =
+                        static_cast<uint16_t>(v[c]);
+            }
+        }
     }
 }
 
@@ -109,23 +148,23 @@ __device__ __forceinline__ void store_cols(uint16_t* p, long long avail,
 // (branch-free), outputs are stored as soon as a pass is done, and the rare
 // out-of-range outputs (value 65536, src/fec_rs_fnt.h:253-269) are found by
 // one OR-reduction per pass and fixed up off the fast path.
+// KEQ: k == K (no zero-padded inputs to mask).
 // ---------------------------------------------------------------------------
-template <int K, int COLS, bool FULL>
+template <int K, int COLS, bool FULL, bool KEQ, bool BUF>
 __device__ __forceinline__ void encode_body(
     int k, int n, int n_out, const int32_t* __restrict__ twist,
-    const uint16_t* __restrict__ src, long long drs, uint16_t* __restrict__ dst,
-    long long ors, long long col, long long avail, int s, const Oor& oor)
+    const Region<BUF>& gi, uint32_t irs, const Region<BUF>& go, uint32_t ors,
+    uint32_t voff, long long col, long long avail, int s, const Oor& oor)
 {
-    const bool rec = oor.counts != nullptr;
     int32_t x[COLS][K];
 #pragma unroll
     for (int t = 0; t < K; t++) {
-        const int row = t < k ? t : k - 1;  // branch-free: clamp, then mask
+        const int row = KEQ ? t : (t < k ? t : k - 1);  // clamp, then mask
         int32_t v[COLS];
-        load_cols<COLS, FULL>(src + row * drs, avail, v);
+        ld<COLS, FULL, BUF>(gi, static_cast<uint32_t>(row) * irs, voff, avail, v);
 #pragma unroll
         for (int c = 0; c < COLS; c++)
-            x[c][t] = t < k ? v[c] : 0;
+            x[c][t] = (KEQ || t < k) ? v[c] : 0;
     }
 
     const int passes = n / K;
@@ -149,7 +188,7 @@ __device__ __forceinline__ void encode_body(
                 const int32_t cb = tw[t];
 #pragma unroll
                 for (int c = 0; c < COLS; c++)
-                    y[c][t] = t == 0 ? x[c][t] : fold(x[c][t] * cb);
+                    y[c][t] = t == 0 ? x[c][t] : fold(mul_i24_s(x[c][t], cb));
             }
 #pragma unroll
             for (int c = 0; c < COLS; c++)
@@ -169,53 +208,67 @@ __device__ __forceinline__ void encode_body(
                 bad |= o[c];
             }
             if (row < n_out)
-                store_cols<COLS, FULL>(dst + row * ors, avail, o);
+                st<COLS, FULL, BUF>(go, static_cast<uint32_t>(row) * ors, voff,
+                                    avail, o);
         }
         if (__builtin_expect((bad >> 16) != 0, 0)) {
+            // fix the stored words of this pass, then record the OOR marks
+            // from a bitmask (keeps the atomics out of the unrolled code)
+            uint64_t mark = 0;
 #pragma unroll
             for (int u = 0; u < K; u++) {
                 const int row = passes * u + v;
-                bool any = false;
+                uint32_t any = 0;
                 uint32_t o[COLS];
 #pragma unroll
                 for (int c = 0; c < COLS; c++) {
                     const uint32_t cv = canon_v(y[c][u]);
                     o[c] = cv & 0xffffu;
-                    if (static_cast<uint32_t>(y[c][u]) > 65535u && row < n_out) {
-                        any = true;
-                        if (rec && cv == 65536u && c < avail)
-                            record_oor(oor, s, row, col + c);
-                    }
+                    any |= static_cast<uint32_t>(y[c][u]) >> 16;
+                    if (cv == 65536u && (FULL || c < avail))
+                        mark |= 1ull << (u * COLS + c);
                 }
-                if (any)
-                    store_cols<COLS, FULL>(dst + row * ors, avail, o);
+                if (any && row < n_out)
+                    st<COLS, FULL, BUF>(go, static_cast<uint32_t>(row) * ors,
+                                        voff, avail, o);
+            }
+            if (oor.counts) {
+                while (mark) {
+                    const int b = __builtin_ctzll(mark);
+                    mark &= mark - 1;
+                    const int row = passes * (b / COLS) + v;
+                    if (row < n_out)
+                        record_oor(oor, s, row, col + (b % COLS));
+                }
             }
         }
     }
 }
 
-template <int K, int COLS>
+template <int K, int COLS, bool KEQ, bool BUF>
 __global__ __launch_bounds__(kBlock) void encode_fnt_kernel(
     int k, int n, int n_out, const int32_t* __restrict__ twist,
-    const uint16_t* __restrict__ data, long long dss, long long drs,
-    uint16_t* __restrict__ out, long long oss, long long ors, long long words,
-    int tiles, Oor oor)
+    const uint16_t* __restrict__ data, long long dss, uint32_t irs,
+    uint32_t iext, uint16_t* __restrict__ out, long long oss, uint32_t ors,
+    uint32_t oext, long long words, int tiles, Oor oor)
 {
     const int b = blockIdx.x;
     const int s = b / tiles;
     const int tile = b - s * tiles;
     const long long col0 = static_cast<long long>(tile) * kBlock * COLS;
     const long long col = col0 + static_cast<long long>(threadIdx.x) * COLS;
-    const uint16_t* src = data + s * dss + col;
-    uint16_t* dst = out + s * oss + col;
+    const Region<BUF> gi(data + s * dss, iext);
+    const Region<BUF> go(out + s * oss, oext);
+    const uint32_t voff = static_cast<uint32_t>(col * 2);
     if (col0 + kBlock * COLS <= words) {  // block-uniform
-        encode_body<K, COLS, true>(k, n, n_out, twist, src, drs, dst, ors, col,
-                                   COLS, s, oor);
+        encode_body<K, COLS, true, KEQ, BUF>(k, n, n_out, twist, gi, irs, go,
+                                             ors, voff, col, COLS, s, oor);
     } else {
         if (col >= words)
             return;
-        encode_body<K, COLS, false>(k, n, n_out, twist, src, drs, dst, ors,
-                                    col, words - col, s, oor);
+        encode_body<K, COLS, false, KEQ, BUF>(k, n, n_out, twist, gi, irs, go,
+                                              ors, voff, col, words - col, s,
+                                              oor);
     }
 }
 
@@ -229,10 +282,17 @@ __global__ __launch_bounds__(kBlock) void encode_fnt_kernel(
 constexpr int kMaxTileOor = 256;
 typedef short qi_short2 __attribute__((ext_vector_type(2)));
 
-template <int KP, int COLS, bool FULL>
+// byte extents of the stripe regions a matrix launch touches
+struct MatExt {
+    uint32_t e0, e1, eo;
+};
+
+template <int KP, int COLS, bool FULL, bool BUF>
 __device__ __forceinline__ void matrix_load(int kin, const uint16_t* sid,
-                                            const RowSrc& src, long long col,
-                                            long long avail, int s,
+                                            const RowSrc& src,
+                                            const Region<BUF>& g0,
+                                            const Region<BUF>& g1, uint32_t voff,
+                                            long long avail,
                                             int32_t (&xp)[COLS][KP])
 {
     // every received row, branch-free (rows past kin are masked to 0), then
@@ -245,10 +305,13 @@ __device__ __forceinline__ void matrix_load(int kin, const uint16_t* sid,
             const int i = 2 * j + h;
             const int ii = i < kin ? i : kin - 1;
             const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
-            const uint16_t* p =
-                id < src.split ? src.base0 + s * src.ss0 + id * src.rs0
-                               : src.base1 + s * src.ss1 + (id - src.split) * src.rs1;
-            load_cols<COLS, FULL>(p + col, avail, vv[h]);
+            if (id < src.split)
+                ld<COLS, FULL, BUF>(g0, static_cast<uint32_t>(id * src.rs0 * 2),
+                                    voff, avail, vv[h]);
+            else
+                ld<COLS, FULL, BUF>(
+                    g1, static_cast<uint32_t>((id - src.split) * src.rs1 * 2), voff,
+                    avail, vv[h]);
 #pragma unroll
             for (int c = 0; c < COLS; c++)
                 vv[h][c] = i < kin ? vv[h][c] : 0;
@@ -256,18 +319,18 @@ __device__ __forceinline__ void matrix_load(int kin, const uint16_t* sid,
 #pragma unroll
         for (int c = 0; c < COLS; c++)
             xp[c][j] = static_cast<int32_t>(
-                (static_cast<uint32_t>(vv[0][c]) |
-                 (static_cast<uint32_t>(vv[1][c]) << 16)) ^
+                pack_lo(static_cast<uint32_t>(vv[0][c]),
+                        static_cast<uint32_t>(vv[1][c])) ^
                 0x80008000u);
     }
 }
 
-template <int KP, int COLS, bool FULL>
+template <int KP, int COLS, bool FULL, bool BUF>
 __device__ __forceinline__ void matrix_compute(
     const MatLayout& L, const int32_t* sm, const int32_t* __restrict__ plain,
-    const int32_t (&xp)[COLS][KP], uint16_t* __restrict__ obase, long long ors,
-    long long col, long long avail, int s, int n_marks, const int* s_i,
-    const uint32_t* s_col, const Oor& out_oor)
+    const int32_t (&xp)[COLS][KP], const Region<BUF>& go, uint32_t ors,
+    uint32_t voff, long long col, long long avail, int s, int n_marks,
+    const int* s_i, const uint32_t* s_col, const Oor& out_oor)
 {
     // sm: the packed matrix, kcorr and rscale staged in LDS
     const int kin = L.kin;
@@ -319,20 +382,22 @@ __device__ __forceinline__ void matrix_compute(
         if (__builtin_expect((bad >> 16) != 0, 0)) {
 #pragma unroll
             for (int c = 0; c < COLS; c++) {
-                if (static_cast<uint32_t>(y[c]) > 65535u && rec && c < avail)
+                if (static_cast<uint32_t>(y[c]) > 65535u && rec &&
+                    (FULL || c < avail))
                     record_oor(out_oor, s, t, col + c);
                 o[c] = fix16(y[c]);
             }
         }
-        store_cols<COLS, FULL>(obase + t * ors, avail, o);
+        st<COLS, FULL, BUF>(go, static_cast<uint32_t>(t) * ors, voff, avail, o);
     }
 }
 
-template <int KP, int COLS>
+template <int KP, int COLS, bool BUF>
 __global__ __launch_bounds__(kBlock) void matrix_kernel(
     MatLayout L, const int32_t* __restrict__ mat, long long mat_stride,
-    const uint16_t* __restrict__ ids, RowSrc src, RowDst dst, long long words,
-    int tiles, Oor in_oor, int slot_base, Oor out_oor, uint32_t* err)
+    const uint16_t* __restrict__ ids, RowSrc src, RowDst dst, MatExt ext,
+    long long words, int tiles, Oor in_oor, int slot_base, Oor out_oor,
+    uint32_t* err)
 {
     extern __shared__ int32_t s_mat[];  // packed + kcorr + rscale
     __shared__ int s_cnt;
@@ -345,16 +410,22 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
     const int kin = L.kin;
     const long long col0 = static_cast<long long>(tile) * kBlock * COLS;
     const long long col = col0 + static_cast<long long>(threadIdx.x) * COLS;
+    const uint32_t voff = static_cast<uint32_t>(col * 2);
     const int32_t* M = mat + s * mat_stride;
     const uint16_t* sid = ids ? ids + static_cast<long long>(s) * kin : nullptr;
     const bool full = col0 + kBlock * COLS <= words;  // block-uniform
+    const Region<BUF> g0(src.base0 + s * src.ss0, ext.e0);
+    const Region<BUF> g1(src.base1 ? src.base1 + s * src.ss1 : src.base0,
+                         ext.e1);
+    const Region<BUF> go(dst.base + s * dst.ss, ext.eo);
 
     // 1) issue every row load of this lane first
     int32_t xp[COLS][KP];
     if (full) {
-        matrix_load<KP, COLS, true>(kin, sid, src, col, COLS, s, xp);
+        matrix_load<KP, COLS, true, BUF>(kin, sid, src, g0, g1, voff, COLS, xp);
     } else if (col < words) {
-        matrix_load<KP, COLS, false>(kin, sid, src, col, words - col, s, xp);
+        matrix_load<KP, COLS, false, BUF>(kin, sid, src, g0, g1, voff,
+                                          words - col, xp);
     }
     // 2) meanwhile stage the matrix rows in LDS and gather this tile's OOR
     //    marks of the received rows (decode_prepare, src/fec_base.h:1361-1404)
@@ -364,7 +435,6 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
     if (threadIdx.x == 0)
         s_cnt = 0;
     __syncthreads();
-    int n_marks = 0;
     if (in_oor.counts) {
         const long long col1 = col0 + kBlock * COLS;
         for (int i = threadIdx.x; i < kin; i += kBlock) {
@@ -391,16 +461,17 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
         }
     }
     __syncthreads();
-    n_marks = min(s_cnt, kMaxTileOor);
-    uint16_t* obase = dst.base + s * dst.ss + col;
+    const int n_marks = min(s_cnt, kMaxTileOor);
     const int32_t* plain = M + L.plain();
+    const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
     if (full) {
-        matrix_compute<KP, COLS, true>(L, s_mat, plain, xp, obase, dst.rs, col,
-                                       COLS, s, n_marks, s_i, s_col, out_oor);
+        matrix_compute<KP, COLS, true, BUF>(L, s_mat, plain, xp, go, ors, voff,
+                                            col, COLS, s, n_marks, s_i, s_col,
+                                            out_oor);
     } else if (col < words) {
-        matrix_compute<KP, COLS, false>(L, s_mat, plain, xp, obase, dst.rs, col,
-                                        words - col, s, n_marks, s_i, s_col,
-                                        out_oor);
+        matrix_compute<KP, COLS, false, BUF>(L, s_mat, plain, xp, go, ors, voff,
+                                             col, words - col, s, n_marks, s_i,
+                                             s_col, out_oor);
     }
 }
 
@@ -494,18 +565,30 @@ static int grid_for(long long words, int cols, int n_stripes, int* tiles)
     return 0;
 }
 
-template <int K, int COLS>
+// byte extent of `rows` rows of `words` u16 at row stride rs (elements);
+// 0 when it does not fit a 32-bit buffer range
+static uint32_t extent(long long rows, long long rs, long long words)
+{
+    if (rows <= 0)
+        return 0;
+    const long long e = ((rows - 1) * rs + words) * 2;
+    return e > 0 && e < 0x7fffffffLL ? static_cast<uint32_t>(e) : 0;
+}
+
+template <int K, int COLS, bool KEQ, bool BUF>
 static int enc_launch(int k, int n, int n_out, const int32_t* tw,
                       const uint16_t* data, long long dss, long long drs,
-                      RowDst out, long long words, int S, Oor oor,
-                      hipStream_t st)
+                      uint32_t iext, RowDst out, uint32_t oext, long long words,
+                      int S, Oor oor, hipStream_t st)
 {
     int tiles;
     if (grid_for(words, COLS, S, &tiles))
         return -1;
-    hipLaunchKernelGGL((encode_fnt_kernel<K, COLS>), dim3(tiles * S),
-                       dim3(kBlock), 0, st, k, n, n_out, tw, data, dss, drs,
-                       out.base, out.ss, out.rs, words, tiles, oor);
+    hipLaunchKernelGGL((encode_fnt_kernel<K, COLS, KEQ, BUF>), dim3(tiles * S),
+                       dim3(kBlock), 0, st, k, n, n_out, tw, data, dss,
+                       static_cast<uint32_t>(drs * 2), iext, out.base, out.ss,
+                       static_cast<uint32_t>(out.rs * 2), oext, words, tiles,
+                       oor);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -525,12 +608,41 @@ int launch_encode_fnt(int k, int n, int n_out, const int32_t* d_twist,
     const int K = static_cast<int>(ceil2(static_cast<uint32_t>(k)));
     const bool a2 = aligned_for(2, data, dss, drs, out.ss, out.rs) &&
                     (reinterpret_cast<uintptr_t>(out.base) % 4) == 0;
-#define QI_ENC(KK, C2)                                                        \
-    if (K == KK)                                                              \
-        return a2 ? enc_launch<KK, C2>(k, n, n_out, d_twist, data, dss, drs,  \
-                                       out, words, S, oor, st)                \
-                  : enc_launch<KK, 1>(k, n, n_out, d_twist, data, dss, drs,   \
-                                      out, words, S, oor, st);
+    const uint32_t ie = extent(k, drs, words), oe = extent(n_out, out.rs, words);
+    if (!ie || !oe) {
+        // stripes wider than a 31-bit buffer range: flat addressing
+        switch (K) {
+#define QI_ENC_FLAT(KK)                                                        \
+    case KK:                                                                   \
+        return enc_launch<KK, 1, false, false>(k, n, n_out, d_twist, data, dss, \
+                                               drs, 0, out, 0, words, S, oor,  \
+                                               st);
+            QI_ENC_FLAT(1)
+            QI_ENC_FLAT(2)
+            QI_ENC_FLAT(4)
+            QI_ENC_FLAT(8)
+            QI_ENC_FLAT(16)
+            QI_ENC_FLAT(32)
+            QI_ENC_FLAT(64)
+#undef QI_ENC_FLAT
+        default:
+            return -3;
+        }
+    }
+#define QI_ENC(KK, C2)                                                         \
+    if (K == KK) {                                                             \
+        if (a2 && k == KK)                                                     \
+            return enc_launch<KK, C2, true, true>(k, n, n_out, d_twist, data,  \
+                                                  dss, drs, ie, out, oe,       \
+                                                  words, S, oor, st);          \
+        if (a2)                                                                \
+            return enc_launch<KK, C2, false, true>(k, n, n_out, d_twist, data, \
+                                                   dss, drs, ie, out, oe,      \
+                                                   words, S, oor, st);         \
+        return enc_launch<KK, 1, false, true>(k, n, n_out, d_twist, data, dss, \
+                                              drs, ie, out, oe, words, S, oor, \
+                                              st);                             \
+    }
     QI_ENC(1, 2)
     QI_ENC(2, 2)
     QI_ENC(4, 2)
@@ -560,9 +672,9 @@ int matrix_kp(int kin)
     return -1;
 }
 
-template <int KP, int COLS>
+template <int KP, int COLS, bool BUF>
 static int mat_launch(const MatLayout& L, const int32_t* mat, long long ms,
-                      const uint16_t* ids, RowSrc src, RowDst dst,
+                      const uint16_t* ids, RowSrc src, RowDst dst, MatExt ext,
                       long long words, int S, Oor in_oor, int slot_base,
                       Oor out_oor, uint32_t* err, hipStream_t st)
 {
@@ -572,9 +684,9 @@ static int mat_launch(const MatLayout& L, const int32_t* mat, long long ms,
     const size_t lds = L.plain() * sizeof(int32_t);
     if (lds > 64 * 1024)
         return -5;
-    hipLaunchKernelGGL((matrix_kernel<KP, COLS>), dim3(tiles * S), dim3(kBlock),
-                       lds, st, L, mat, ms, ids, src, dst, words, tiles, in_oor,
-                       slot_base, out_oor, err);
+    hipLaunchKernelGGL((matrix_kernel<KP, COLS, BUF>), dim3(tiles * S),
+                       dim3(kBlock), lds, st, L, mat, ms, ids, src, dst, ext,
+                       words, tiles, in_oor, slot_base, out_oor, err);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -592,12 +704,24 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
                     (reinterpret_cast<uintptr_t>(dst.base) % 4) == 0;
     if (L.KP != matrix_kp(L.kin))
         return -4;
-#define QI_MAT(KK)                                                            \
-    if (L.KP == KK)                                                           \
-        return a2 ? mat_launch<KK, 2>(L, mat, ms, ids, src, dst, words, S, io, \
-                                      slot_base, oo, err, st)                 \
-                  : mat_launch<KK, 1>(L, mat, ms, ids, src, dst, words, S, io, \
-                                      slot_base, oo, err, st);
+    MatExt ext{extent(src.rows0, src.rs0, words),
+               extent(src.rows1, src.rs1, words),
+               extent(L.R, dst.rs, words)};
+    const bool buf = ext.e0 && ext.eo && (!src.base1 || ext.e1);
+#define QI_MAT(KK)                                                             \
+    if (L.KP == KK) {                                                          \
+        if (!buf)                                                              \
+            return mat_launch<KK, 1, false>(L, mat, ms, ids, src, dst, ext,     \
+                                            words, S, io, slot_base, oo, err,  \
+                                            st);                               \
+        return (a2 && KK <= 16)                                                \
+                   ? mat_launch<KK, 2, true>(L, mat, ms, ids, src, dst, ext,   \
+                                             words, S, io, slot_base, oo, err, \
+                                             st)                               \
+                   : mat_launch<KK, 1, true>(L, mat, ms, ids, src, dst, ext,   \
+                                             words, S, io, slot_base, oo, err, \
+                                             st);                              \
+    }
     QI_MAT(2)
     QI_MAT(4)
     QI_MAT(8)

@@ -52,7 +52,7 @@ int qi_gpu_encode(qi_plan* p, const uint16_t* d_data, long long dss,
         return launch_encode_fnt(p->k, p->n, p->n_outputs, p->d_twist, d_data,
                                  dss, drs, out, words, n_stripes, oor,
                                  p->d_err, st(stream));
-    RowSrc src{d_data, dss, drs, 1 << 30, nullptr, 0, 0, 0};
+    RowSrc src{d_data, dss, drs, 1 << 30, nullptr, 0, 0, 0, p->k, 0};
     return launch_matrix(p->gen, p->d_gen, 0, nullptr, src, out, words,
                          n_stripes, nullptr, 0, d_counts ? &oor : nullptr,
                          p->d_err, st(stream));
@@ -115,9 +115,10 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
     const MatLayout L = ctx_layout(p);
     RowSrc src;
     if (p->sys)
-        src = RowSrc{d_data ? d_data : d_coded, dss, drs, p->k, d_coded, css, crs, 0};
+        src = RowSrc{d_data ? d_data : d_coded, dss, drs, p->k, d_coded, css, crs, 0,
+                     p->k, p->n_outputs};
     else
-        src = RowSrc{d_coded, css, crs, 1 << 30, nullptr, 0, 0, 0};
+        src = RowSrc{d_coded, css, crs, 1 << 30, nullptr, 0, 0, 0, p->n_outputs, 0};
     Oor in{const_cast<uint32_t*>(d_counts), const_cast<uint32_t*>(d_entries),
            p->n_outputs, cap};
     RowDst out{d_out, oss, ors};

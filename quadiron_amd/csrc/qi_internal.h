@@ -37,6 +37,7 @@ struct RowSrc {
     const uint16_t* base1;
     long long ss1, rs1;
     int by_pos;
+    int rows0, rows1;  // rows addressable through base0 / base1
 };
 
 // Output rows: row t of stripe s at base + s*ss + t*rs
