@@ -110,7 +110,7 @@ def main():
     # per-stripe erasure pattern: keep a random k-subset of the n ids
     perm = torch.rand((S, k + m), device=dev, generator=g).argsort(dim=1)
     ids = perm[:, :k].sort(dim=1).values.to(torch.int16).contiguous()
-    ctx = torch.empty(plan.ctx_bytes(S), dtype=torch.uint8, device=dev)
+    ctx = torch.empty(plan.ctx_bytes(S, P), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
 
     ev = []
@@ -125,7 +125,7 @@ def main():
         plan.encode(data, coded, counts, entries, cap, stream=stream)
         if timed:
             e1.record()
-        plan.decode_ctx(ids, ctx, stream=stream)
+        plan.decode_ctx(ids, ctx, P, counts, entries, cap, stream=stream)
         plan.decode(ctx, ids, coded, dec, counts=counts, entries=entries,
                     cap=cap, stream=stream)
         if timed:

@@ -62,17 +62,23 @@ int qi_gpu_encode(qi_plan* plan, const uint16_t* d_data,
                   uint32_t* d_oor_counts, uint32_t* d_oor_entries, int oor_cap,
                   void* stream);
 
-/* Bytes of device workspace for n_stripes decode contexts. */
-size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes);
+/* Bytes of device workspace for n_stripes decode contexts of `words`
+ * columns each. */
+size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
+                               long long words);
 
 /* Build per-stripe decode contexts from the received fragment ids:
  * d_ids[s*k + i] (u16, ascending, distinct, < k+m) -- the k fragments the
  * decoder uses (FecCode::decode_blocks_vertical picks the first k present,
- * src/fec_base.h:1199-1236).  k <= 64 on the device; larger k are built on
- * the host from h_ids (may be NULL when k <= 64). */
+ * src/fec_base.h:1199-1236) -- and route the OOR marks of those fragments
+ * (buckets as produced by qi_gpu_encode; NULL counts = none) into per-tile
+ * tables.  k <= 64 on the device; larger k are built on the host from h_ids
+ * (may be NULL when k <= 64). */
 int qi_gpu_decode_ctx(qi_plan* plan, const uint16_t* d_ids,
-                      const uint16_t* h_ids, int n_stripes, void* d_ctx,
-                      void* stream);
+                      const uint16_t* h_ids, int n_stripes,
+                      const uint32_t* d_oor_counts,
+                      const uint32_t* d_oor_entries, int oor_cap,
+                      long long words, void* d_ctx, void* stream);
 
 /* Batch decode.  Received fragment id f of stripe s is read from
  *   f <  k (systematic data rows):  d_data + s*dss + f*drs

@@ -44,8 +44,8 @@ def _declare(lib):
         "qi_plan_n_outputs": (I, [V]),
         "qi_gpu_oor_clear": (I, [V, SZ, V]),
         "qi_gpu_encode": (I, [V, V, LL, LL, V, LL, LL, LL, I, V, V, I, V]),
-        "qi_gpu_decode_ctx_bytes": (SZ, [V, I]),
-        "qi_gpu_decode_ctx": (I, [V, V, V, I, V, V]),
+        "qi_gpu_decode_ctx_bytes": (SZ, [V, I, LL]),
+        "qi_gpu_decode_ctx": (I, [V, V, V, I, V, V, I, LL, V, V]),
         "qi_gpu_decode": (I, [V, V, V, V, LL, LL, V, LL, LL, V, V, I, V, LL,
                               LL, LL, I, V]),
         "qi_gpu_take_error": (I, [V]),
@@ -138,15 +138,20 @@ class Plan:
         if rc:
             raise RuntimeError(f"qi_gpu_encode failed: {rc}")
 
-    def ctx_bytes(self, n_stripes):
-        return lib().qi_gpu_decode_ctx_bytes(self.h, n_stripes)
+    def ctx_bytes(self, n_stripes, words):
+        return lib().qi_gpu_decode_ctx_bytes(self.h, n_stripes, words)
 
-    def decode_ctx(self, ids, ctx, h_ids=None, stream=None):
-        """ids: int16 tensor [S, k] on cuda (fragment ids)."""
+    def decode_ctx(self, ids, ctx, words, counts=None, entries=None, cap=0,
+                   h_ids=None, stream=None):
+        """ids: int16 tensor [S, k] on cuda (fragment ids); OOR buckets of
+        the coded rows as produced by encode (routed into the contexts)."""
         rc = lib().qi_gpu_decode_ctx(
             self.h, ids.data_ptr(),
             h_ids.ctypes.data_as(C.c_void_p) if h_ids is not None else None,
-            ids.shape[0], ctx.data_ptr(), self._stream(stream))
+            ids.shape[0],
+            counts.data_ptr() if counts is not None else None,
+            entries.data_ptr() if entries is not None else None, int(cap),
+            words, ctx.data_ptr(), self._stream(stream))
         if rc:
             raise RuntimeError(f"qi_gpu_decode_ctx failed: {rc}")
 

@@ -247,7 +247,8 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
     std::vector<uint16_t> hids(k);
     for (int i = 0; i < k; i++)
         hids[i] = static_cast<uint16_t>(ids[i]);
-    const size_t ctx_bytes = qi_gpu_decode_ctx_bytes(plan_, 1);
+    const size_t ctx_bytes =
+        qi_gpu_decode_ctx_bytes(plan_, 1, static_cast<long long>(words));
     const size_t cnt_off = 0, ent_off = 64 * ((k * 4 + 63) / 64);
     if (!h.in.reserve(static_cast<size_t>(k) * P * 2) ||
         !h.out.reserve(static_cast<size_t>(k) * P * 2) ||
@@ -269,20 +270,21 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
           "H2D");
     check(hipMemcpyAsync(h.ids.p, hids.data(), k * 2, hipMemcpyHostToDevice, s),
           "H2D");
-    check_rc(qi_gpu_decode_ctx(plan_, static_cast<uint16_t*>(h.ids.p),
-                               hids.data(), 1, h.ctx.p, s),
-             "qi_gpu_decode_ctx");
     // received rows staged by position; OOR buckets by position
-    const MatLayout L{k, k, matrix_kp(k)};
-    RowSrc src{din, 0, static_cast<long long>(P), 1 << 30, nullptr, 0, 0, 1, k, 0};
-    RowDst dst{dout, 0, static_cast<long long>(P)};
     Oor in{reinterpret_cast<uint32_t*>(dcb + cnt_off),
            reinterpret_cast<uint32_t*>(dcb + ent_off), k,
            static_cast<int>(cap)};
-    check_rc(launch_matrix(L, static_cast<const int32_t*>(h.ctx.p), 0,
-                           static_cast<uint16_t*>(h.ids.p), src, dst,
+    check_rc(build_ctx(plan_, static_cast<uint16_t*>(h.ids.p), hids.data(), 1,
+                       &in, 0, 1, static_cast<long long>(words), h.ctx.p, s),
+             "decode context");
+    const MatLayout L{k, k, matrix_kp(k)};
+    RowSrc src{din, 0, static_cast<long long>(P), 1 << 30, nullptr, 0, 0, 1, k, 0};
+    RowDst dst{dout, 0, static_cast<long long>(P)};
+    const int32_t* ctx = static_cast<const int32_t*>(h.ctx.p);
+    check_rc(launch_matrix(L, ctx, 0, ctx + L.words(), 0, src, dst,
                            static_cast<long long>(words), 1, &in, 0, nullptr,
-                           plan_->d_err, s),
+                           reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
+                           0, plan_->d_err, s),
              "decode");
     for (int t = 0; t < k; t++)
         if (outputs[t])

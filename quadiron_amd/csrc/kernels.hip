@@ -288,7 +288,7 @@ struct MatExt {
 };
 
 template <int KP, int COLS, bool FULL, bool BUF>
-__device__ __forceinline__ void matrix_load(int kin, const uint16_t* sid,
+__device__ __forceinline__ void matrix_load(int kin, const int (&idv)[2 * KP],
                                             const RowSrc& src,
                                             const Region<BUF>& g0,
                                             const Region<BUF>& g1, uint32_t voff,
@@ -303,15 +303,17 @@ __device__ __forceinline__ void matrix_load(int kin, const uint16_t* sid,
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int i = 2 * j + h;
-            const int ii = i < kin ? i : kin - 1;
-            const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
-            if (id < src.split)
-                ld<COLS, FULL, BUF>(g0, static_cast<uint32_t>(id * src.rs0 * 2),
-                                    voff, avail, vv[h]);
-            else
-                ld<COLS, FULL, BUF>(
-                    g1, static_cast<uint32_t>((id - src.split) * src.rs1 * 2), voff,
-                    avail, vv[h]);
+            const int id = src.by_pos ? (i < kin ? i : kin - 1) : idv[i];
+            // branch-free source select (uniform s_cselect): a branch here
+            // makes the compiler drain vmcnt after every row load
+            const bool lo = id < src.split;
+            Region<BUF> g = g0;
+            if constexpr (BUF)
+                g.r = lo ? g0.r : g1.r;
+            g.p = lo ? g0.p : g1.p;
+            const uint32_t off = static_cast<uint32_t>(
+                lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
+            ld<COLS, FULL, BUF>(g, off, voff, avail, vv[h]);
 #pragma unroll
             for (int c = 0; c < COLS; c++)
                 vv[h][c] = i < kin ? vv[h][c] : 0;
@@ -327,18 +329,22 @@ __device__ __forceinline__ void matrix_load(int kin, const uint16_t* sid,
 
 template <int KP, int COLS, bool FULL, bool BUF>
 __device__ __forceinline__ void matrix_compute(
-    const MatLayout& L, const int32_t* sm, const int32_t* __restrict__ plain,
+    const MatLayout& L, const int32_t* __restrict__ M,
     const int32_t (&xp)[COLS][KP], const Region<BUF>& go, uint32_t ors,
-    uint32_t voff, long long col, long long avail, int s, int n_marks,
-    const int* s_i, const uint32_t* s_col, const Oor& out_oor)
+    uint32_t voff, long long col, long long col0, long long avail, int s,
+    int n_rm, const uint32_t* rm, int n_lm, const int* s_i,
+    const uint32_t* s_col, const Oor& out_oor)
 {
-    // sm: the packed matrix, kcorr and rscale staged in LDS
+    // M: the per-stripe matrix block (wave-uniform: scalar loads)
     const int kin = L.kin;
-    const int32_t* kcorr = sm + L.kcorr();
-    const int32_t* rscale = sm + L.rscale();
+    const int32_t* kcorr = M + L.kcorr();
+    const int32_t* rscale = M + L.rscale();
+    const int32_t* plain = M + L.plain();
     const bool rec = out_oor.counts != nullptr;
+    // routed marks are relative to their kRouteTile-column tile
+    const long long rbase = col0 / kRouteTile * kRouteTile;
     for (int t = 0; t < L.R; t++) {
-        const int32_t* mrow = sm + t * KP;
+        const int32_t* mrow = M + t * KP;
         int32_t acc[COLS];
 #pragma unroll
         for (int c = 0; c < COLS; c++)
@@ -355,11 +361,21 @@ __device__ __forceinline__ void matrix_compute(
 #pragma unroll
         for (int c = 0; c < COLS; c++)
             y[c] = fold(acc[c]);  // T-range
-        for (int e = 0; e < n_marks; e++) {
-            // restored symbol is 65536 == -1 where the stored word is 0
-            const long long d = static_cast<long long>(s_col[e]) - col;
+        // restored OOR symbols: 65536 == -1 where the stored word is 0
+        for (int e = 0; e < n_rm + n_lm; e++) {
+            long long w;
+            int pos;
+            if (e < n_rm) {
+                const uint32_t v = rm[e];
+                pos = static_cast<int>(v >> 16);
+                w = rbase + (v & 0xffffu);
+            } else {
+                pos = s_i[e - n_rm];
+                w = s_col[e - n_rm];
+            }
+            const long long d = w - col;
             if (d >= 0 && d < COLS) {
-                const int32_t corr = plain[t * kin + s_i[e]];
+                const int32_t corr = plain[t * kin + pos];
 #pragma unroll
                 for (int c = 0; c < COLS; c++)
                     if (c == d)
@@ -370,7 +386,7 @@ __device__ __forceinline__ void matrix_compute(
         if (rs != 1) {
 #pragma unroll
             for (int c = 0; c < COLS; c++)
-                y[c] = fold(fold(y[c] * rs));
+                y[c] = fold(fold(mul_i24_s(y[c], rs)));
         }
         uint32_t o[COLS];
         uint32_t bad = 0;
@@ -395,11 +411,11 @@ __device__ __forceinline__ void matrix_compute(
 template <int KP, int COLS, bool BUF>
 __global__ __launch_bounds__(kBlock) void matrix_kernel(
     MatLayout L, const int32_t* __restrict__ mat, long long mat_stride,
-    const uint16_t* __restrict__ ids, RowSrc src, RowDst dst, MatExt ext,
-    long long words, int tiles, Oor in_oor, int slot_base, Oor out_oor,
-    uint32_t* err)
+    const int32_t* __restrict__ ids, long long ids_stride, RowSrc src,
+    RowDst dst, MatExt ext, long long words, int tiles, Oor in_oor,
+    int slot_base, Oor out_oor, const uint32_t* __restrict__ route,
+    long long route_stride, uint32_t* err)
 {
-    extern __shared__ int32_t s_mat[];  // packed + kcorr + rscale
     __shared__ int s_cnt;
     __shared__ int s_i[kMaxTileOor];
     __shared__ uint32_t s_col[kMaxTileOor];
@@ -409,34 +425,64 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
     const int tile = b - s * tiles;
     const int kin = L.kin;
     const long long col0 = static_cast<long long>(tile) * kBlock * COLS;
+    const long long col1 = col0 + kBlock * COLS;
     const long long col = col0 + static_cast<long long>(threadIdx.x) * COLS;
     const uint32_t voff = static_cast<uint32_t>(col * 2);
     const int32_t* M = mat + s * mat_stride;
-    const uint16_t* sid = ids ? ids + static_cast<long long>(s) * kin : nullptr;
-    const bool full = col0 + kBlock * COLS <= words;  // block-uniform
+    // fragment ids as dwords (scalar loads; a u16 array would need vector
+    // loads + readfirstlane, draining vmcnt between the row loads)
+    const int32_t* sid = ids ? ids + s * ids_stride : nullptr;
+    const bool full = col1 <= words;  // block-uniform
     const Region<BUF> g0(src.base0 + s * src.ss0, ext.e0);
     const Region<BUF> g1(src.base1 ? src.base1 + s * src.ss1 : src.base0,
                          ext.e1);
     const Region<BUF> go(dst.base + s * dst.ss, ext.eo);
 
-    // 1) issue every row load of this lane first
+    // the OOR marks of the received rows in this tile (decode_prepare,
+    // src/fec_base.h:1361-1404): from the context's route table (scalar
+    // loads, issued with the row loads), or -- when the table overflowed or
+    // is absent -- by scanning the OOR buckets
+    int n_rm = 0;
+    const uint32_t* rm = nullptr;
+    bool scan = in_oor.counts != nullptr;
+    if (route) {
+        const uint32_t* rt =
+            route + s * route_stride + (col0 / kRouteTile) * kRouteStride;
+        const uint32_t rc = rt[0];
+        if (rc <= static_cast<uint32_t>(kRouteCap)) {
+            n_rm = static_cast<int>(rc);
+            rm = rt + 1;
+            scan = false;
+        }
+    }
+
+    // all ids up front: 2*KP dwords (the context pads past kin), so the
+    // scalar loads batch into a few s_load_dwordxN
+    int idv[2 * KP];
+    if (sid) {
+#pragma unroll
+        for (int i = 0; i < 2 * KP; i++)
+            idv[i] = sid[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2 * KP; i++)
+            idv[i] = i;
+    }
+#pragma unroll
+    for (int i = 0; i < 2 * KP; i++)  // clamp rows past kin (masked later)
+        idv[i] = i < kin ? idv[i] : idv[0];
     int32_t xp[COLS][KP];
     if (full) {
-        matrix_load<KP, COLS, true, BUF>(kin, sid, src, g0, g1, voff, COLS, xp);
+        matrix_load<KP, COLS, true, BUF>(kin, idv, src, g0, g1, voff, COLS, xp);
     } else if (col < words) {
-        matrix_load<KP, COLS, false, BUF>(kin, sid, src, g0, g1, voff,
+        matrix_load<KP, COLS, false, BUF>(kin, idv, src, g0, g1, voff,
                                           words - col, xp);
     }
-    // 2) meanwhile stage the matrix rows in LDS and gather this tile's OOR
-    //    marks of the received rows (decode_prepare, src/fec_base.h:1361-1404)
-    const int nm = static_cast<int>(L.plain());
-    for (int i = threadIdx.x; i < nm; i += kBlock)
-        s_mat[i] = M[i];
-    if (threadIdx.x == 0)
-        s_cnt = 0;
-    __syncthreads();
-    if (in_oor.counts) {
-        const long long col1 = col0 + kBlock * COLS;
+    int n_lm = 0;
+    if (scan) {  // block-uniform
+        if (threadIdx.x == 0)
+            s_cnt = 0;
+        __syncthreads();
         for (int i = threadIdx.x; i < kin; i += kBlock) {
             const int id = sid ? sid[i] : i;
             const int slot = (src.by_pos ? i : id) - slot_base;
@@ -459,18 +505,17 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
                 }
             }
         }
+        __syncthreads();
+        n_lm = min(s_cnt, kMaxTileOor);
     }
-    __syncthreads();
-    const int n_marks = min(s_cnt, kMaxTileOor);
-    const int32_t* plain = M + L.plain();
     const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
     if (full) {
-        matrix_compute<KP, COLS, true, BUF>(L, s_mat, plain, xp, go, ors, voff,
-                                            col, COLS, s, n_marks, s_i, s_col,
+        matrix_compute<KP, COLS, true, BUF>(L, M, xp, go, ors, voff, col, col0,
+                                            COLS, s, n_rm, rm, n_lm, s_i, s_col,
                                             out_oor);
     } else if (col < words) {
-        matrix_compute<KP, COLS, false, BUF>(L, s_mat, plain, xp, go, ors, voff,
-                                             col, words - col, s, n_marks, s_i,
+        matrix_compute<KP, COLS, false, BUF>(L, M, xp, go, ors, voff, col, col0,
+                                             words - col, s, n_rm, rm, n_lm, s_i,
                                              s_col, out_oor);
     }
 }
@@ -481,6 +526,8 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
 //   A(x) = prod_j (x - x_j),  Q_i = A / (x - x_i),  A'(x_i) = Q_i(x_i)
 //   mode 0: M[t][i] = coef_t(Q_i) / A'(x_i)       (non-systematic)
 //   mode 1: M[t][i] = Q_i(r^t)   / A'(x_i)        (systematic)
+// plus the OOR route table of the stripe (decode_prepare's props walk,
+// src/fec_base.h:1361-1404, precomputed per tile).
 // One 64-lane workgroup per stripe; k <= 64.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t mulm(uint32_t a, uint32_t b)
@@ -499,18 +546,49 @@ __device__ __forceinline__ uint32_t subm(uint32_t a, uint32_t b)
 
 __global__ __launch_bounds__(64) void decode_ctx_kernel(
     int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
-    int32_t* __restrict__ mat)
+    int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
+    int by_pos, long long words)
 {
     __shared__ uint32_t xs[64];
     __shared__ uint32_t A[65];
     __shared__ uint32_t Mt[64 * 64];
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
-    const long long mstride = static_cast<long long>(L.words());
+    int32_t* mat = ctx + s * ctx_stride;
+    int32_t* cids = mat + L.words();
+    uint32_t* route = reinterpret_cast<uint32_t*>(cids + 2 * L.KP);
+    for (int i = k + tid; i < 2 * L.KP; i += 64)
+        cids[i] = 0;
+    const long long ntiles = route_tiles(words);
 
-    if (tid < k)
-        xs[tid] = powmod_c(r, ids[static_cast<long long>(s) * k + tid]);
+    // route table: clear, then (after the barrier below) fill
+    for (long long t = tid; t < ntiles; t += 64)
+        route[t * kRouteStride] = 0;
+    if (tid < k) {
+        const uint32_t id = ids[static_cast<long long>(s) * k + tid];
+        xs[tid] = powmod_c(r, id);
+        cids[tid] = static_cast<int32_t>(id);
+    }
     __syncthreads();
+    if (in_oor.counts && tid < k) {
+        const int id = ids[static_cast<long long>(s) * k + tid];
+        const int slot = (by_pos ? tid : id) - slot_base;
+        if (slot >= 0) {
+            const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
+            uint32_t c = in_oor.counts[bk];
+            if (c > static_cast<uint32_t>(in_oor.cap))
+                c = in_oor.cap;
+            for (uint32_t e = 0; e < c; e++) {
+                const uint32_t w = in_oor.entries[bk * in_oor.cap + e];
+                if (w >= words)
+                    continue;
+                uint32_t* rt = route + (w / kRouteTile) * kRouteStride;
+                const uint32_t p = atomicAdd(rt, 1u);
+                if (p < static_cast<uint32_t>(kRouteCap))
+                    rt[1 + p] = (static_cast<uint32_t>(tid) << 16) | (w % kRouteTile);
+            }
+        }
+    }
     if (tid == 0) {
         A[0] = 1;
         for (int i = 0; i < k; i++) {
@@ -549,7 +627,7 @@ __global__ __launch_bounds__(64) void decode_ctx_kernel(
     }
     __syncthreads();
     for (int t = tid; t < L.R; t += 64)
-        pack_row(Mt + t * k, k, L.KP, L.R, t, mat + s * mstride);
+        pack_row(Mt + t * k, k, L.KP, L.R, t, mat);
 }
 
 // ---------------------------------------------------------------------------
@@ -674,26 +752,28 @@ int matrix_kp(int kin)
 
 template <int KP, int COLS, bool BUF>
 static int mat_launch(const MatLayout& L, const int32_t* mat, long long ms,
-                      const uint16_t* ids, RowSrc src, RowDst dst, MatExt ext,
+                      const int32_t* ids, long long is, RowSrc src, RowDst dst,
+                      MatExt ext,
                       long long words, int S, Oor in_oor, int slot_base,
-                      Oor out_oor, uint32_t* err, hipStream_t st)
+                      Oor out_oor, const uint32_t* route, long long rstride,
+                      uint32_t* err, hipStream_t st)
 {
     int tiles;
     if (grid_for(words, COLS, S, &tiles))
         return -1;
-    const size_t lds = L.plain() * sizeof(int32_t);
-    if (lds > 64 * 1024)
-        return -5;
     hipLaunchKernelGGL((matrix_kernel<KP, COLS, BUF>), dim3(tiles * S),
-                       dim3(kBlock), lds, st, L, mat, ms, ids, src, dst, ext,
-                       words, tiles, in_oor, slot_base, out_oor, err);
+                       dim3(kBlock), 0, st, L, mat, ms, ids, is, src, dst, ext,
+                       words, tiles, in_oor, slot_base, out_oor, route, rstride,
+                       err);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
-                  const uint16_t* ids, RowSrc src, RowDst dst, long long words,
+                  const int32_t* ids, long long is, RowSrc src, RowDst dst,
+                  long long words,
                   int S, const Oor* in_oor, int slot_base, const Oor* out_oor,
-                  uint32_t* err, hipStream_t st)
+                  const uint32_t* route, long long rstride, uint32_t* err,
+                  hipStream_t st)
 {
     Oor none{nullptr, nullptr, 0, 0};
     Oor io = in_oor ? *in_oor : none;
@@ -711,16 +791,16 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
 #define QI_MAT(KK)                                                             \
     if (L.KP == KK) {                                                          \
         if (!buf)                                                              \
-            return mat_launch<KK, 1, false>(L, mat, ms, ids, src, dst, ext,     \
-                                            words, S, io, slot_base, oo, err,  \
-                                            st);                               \
+            return mat_launch<KK, 1, false>(L, mat, ms, ids, is, src, dst, ext,     \
+                                            words, S, io, slot_base, oo,       \
+                                            route, rstride, err, st);          \
         return (a2 && KK <= 16)                                                \
-                   ? mat_launch<KK, 2, true>(L, mat, ms, ids, src, dst, ext,   \
-                                             words, S, io, slot_base, oo, err, \
-                                             st)                               \
-                   : mat_launch<KK, 1, true>(L, mat, ms, ids, src, dst, ext,   \
-                                             words, S, io, slot_base, oo, err, \
-                                             st);                              \
+                   ? mat_launch<KK, 2, true>(L, mat, ms, ids, is, src, dst, ext,   \
+                                             words, S, io, slot_base, oo,      \
+                                             route, rstride, err, st)          \
+                   : mat_launch<KK, 1, true>(L, mat, ms, ids, is, src, dst, ext,   \
+                                             words, S, io, slot_base, oo,      \
+                                             route, rstride, err, st);         \
     }
     QI_MAT(2)
     QI_MAT(4)
@@ -732,14 +812,17 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
     return -3;
 }
 
-int launch_decode_ctx(int k, int /*n*/, uint32_t r, int mode,
-                      const MatLayout& L, const uint16_t* d_ids, int S,
-                      int32_t* d_mat, hipStream_t st)
+int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
+                      const uint16_t* d_ids, int S, int32_t* d_ctx,
+                      long long ctx_stride, const Oor* in_oor, int slot_base,
+                      int by_pos, long long words, hipStream_t st)
 {
     if (k > 64 || S <= 0)
         return -3;
+    Oor none{nullptr, nullptr, 0, 0};
     hipLaunchKernelGGL(decode_ctx_kernel, dim3(S), dim3(64), 0, st, k, r, mode,
-                       L, d_ids, d_mat);
+                       L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
+                       slot_base, by_pos, words);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -18,12 +18,67 @@ MatLayout ctx_layout(const qi_plan* p)
     return MatLayout{p->k, p->k, matrix_kp(p->k)};
 }
 
+
 hipStream_t st(void* s)
 {
     return static_cast<hipStream_t>(s);
 }
 
 }  // namespace
+
+namespace qi {
+
+long long ctx_stride(const qi_plan* p, long long words)
+{
+    const MatLayout L = ctx_layout(p);
+    return static_cast<long long>(L.words()) + 2 * L.KP +
+           route_tiles(words) * kRouteStride;
+}
+
+// Decode contexts for n_stripes stripes: interpolation matrices + OOR route
+// tables.  k <= 64 on the device; otherwise the matrices are built on the
+// host from h_ids and the route tables are marked "scan the buckets".
+int build_ctx(qi_plan* p, const uint16_t* d_ids, const uint16_t* h_ids,
+              int n_stripes, const Oor* in, int slot_base, int by_pos,
+              long long words, void* d_ctx, hipStream_t s)
+{
+    if (n_stripes == 0)
+        return 0;
+    const MatLayout L = ctx_layout(p);
+    if (L.KP < 0)
+        return -3;
+    const int mode = p->sys ? 1 : 0;
+    const long long cs = ctx_stride(p, words);
+    if (p->k <= 64 && d_ids)
+        return launch_decode_ctx(p->k, p->r, mode, L, d_ids, n_stripes,
+                                 static_cast<int32_t*>(d_ctx), cs, in, slot_base,
+                                 by_pos, words, s);
+    if (!h_ids)
+        return -1;
+    std::vector<int32_t> blk(static_cast<size_t>(cs) * n_stripes, 0);
+    std::vector<uint32_t> ids(p->k), ev(p->k);
+    for (int t = 0; t < p->k; t++)
+        ev[t] = powmod_c(p->r, static_cast<uint32_t>(t));
+    const long long nt = route_tiles(words);
+    for (int s_ = 0; s_ < n_stripes; s_++) {
+        for (int i = 0; i < p->k; i++)
+            ids[i] = h_ids[static_cast<size_t>(s_) * p->k + i];
+        std::vector<uint32_t> M =
+            lagrange_matrix(p->k, p->r, ids.data(), mode, ev.data(), p->k);
+        int32_t* b = blk.data() + cs * s_;
+        pack_matrix(L, M.data(), b);
+        for (int i = 0; i < p->k; i++)
+            b[L.words() + i] = static_cast<int32_t>(ids[i]);
+        for (long long t = 0; t < nt; t++)
+            b[L.words() + 2 * L.KP + t * kRouteStride] = kRouteCap + 1;  // scan
+    }
+    if (hipMemcpyAsync(d_ctx, blk.data(), blk.size() * 4, hipMemcpyHostToDevice,
+                       s) != hipSuccess)
+        return -2;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -2;
+}
+
+}  // namespace qi
 
 extern "C" {
 
@@ -53,52 +108,31 @@ int qi_gpu_encode(qi_plan* p, const uint16_t* d_data, long long dss,
                                  dss, drs, out, words, n_stripes, oor,
                                  p->d_err, st(stream));
     RowSrc src{d_data, dss, drs, 1 << 30, nullptr, 0, 0, 0, p->k, 0};
-    return launch_matrix(p->gen, p->d_gen, 0, nullptr, src, out, words,
+    return launch_matrix(p->gen, p->d_gen, 0, nullptr, 0, src, out, words,
                          n_stripes, nullptr, 0, d_counts ? &oor : nullptr,
-                         p->d_err, st(stream));
+                         nullptr, 0, p->d_err, st(stream));
 }
 
-size_t qi_gpu_decode_ctx_bytes(const qi_plan* p, int n_stripes)
+size_t qi_gpu_decode_ctx_bytes(const qi_plan* p, int n_stripes,
+                               long long words)
 {
-    if (!p || n_stripes < 0)
+    if (!p || n_stripes < 0 || words < 0)
         return 0;
-    return ctx_layout(p).words() * sizeof(int32_t) *
+    return static_cast<size_t>(ctx_stride(p, words)) * sizeof(int32_t) *
            static_cast<size_t>(n_stripes);
 }
 
-int qi_gpu_decode_ctx(qi_plan* p, const uint16_t* d_ids,
-                      const uint16_t* h_ids, int n_stripes, void* d_ctx,
-                      void* stream)
+int qi_gpu_decode_ctx(qi_plan* p, const uint16_t* d_ids, const uint16_t* h_ids,
+                      int n_stripes, const uint32_t* d_counts,
+                      const uint32_t* d_entries, int cap, long long words,
+                      void* d_ctx, void* stream)
 {
-    if (!p || !d_ctx || n_stripes < 0)
+    if (!p || !d_ctx || n_stripes < 0 || words < 0)
         return -1;
-    if (n_stripes == 0)
-        return 0;
-    const MatLayout L = ctx_layout(p);
-    if (L.KP < 0)
-        return -3;
-    const int mode = p->sys ? 1 : 0;
-    if (p->k <= 64 && d_ids)
-        return launch_decode_ctx(p->k, p->n, p->r, mode, L, d_ids, n_stripes,
-                                 static_cast<int32_t*>(d_ctx), st(stream));
-    if (!h_ids)
-        return -1;
-    // host build (k > 64): same Lagrange form as the device kernel
-    std::vector<int32_t> blk(L.words() * static_cast<size_t>(n_stripes));
-    std::vector<uint32_t> ids(p->k), ev(p->k);
-    for (int t = 0; t < p->k; t++)
-        ev[t] = qi::powmod_c(p->r, static_cast<uint32_t>(t));
-    for (int s = 0; s < n_stripes; s++) {
-        for (int i = 0; i < p->k; i++)
-            ids[i] = h_ids[static_cast<size_t>(s) * p->k + i];
-        std::vector<uint32_t> M =
-            lagrange_matrix(p->k, p->r, ids.data(), mode, ev.data(), p->k);
-        pack_matrix(L, M.data(), blk.data() + L.words() * s);
-    }
-    if (hipMemcpyAsync(d_ctx, blk.data(), blk.size() * 4, hipMemcpyHostToDevice,
-                       st(stream)) != hipSuccess)
-        return -2;
-    return hipStreamSynchronize(st(stream)) == hipSuccess ? 0 : -2;
+    Oor in{const_cast<uint32_t*>(d_counts), const_cast<uint32_t*>(d_entries),
+           p->n_outputs, cap};
+    return qi::build_ctx(p, d_ids, h_ids, n_stripes, d_counts ? &in : nullptr,
+                         p->sys ? p->k : 0, 0, words, d_ctx, st(stream));
 }
 
 int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
@@ -122,10 +156,14 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
     Oor in{const_cast<uint32_t*>(d_counts), const_cast<uint32_t*>(d_entries),
            p->n_outputs, cap};
     RowDst out{d_out, oss, ors};
-    return launch_matrix(L, static_cast<const int32_t*>(d_ctx),
-                         static_cast<long long>(L.words()), d_ids, src, out,
-                         words, n_stripes, d_counts ? &in : nullptr,
-                         p->sys ? p->k : 0, nullptr, p->d_err, st(stream));
+    const long long cs = ctx_stride(p, words);
+    const int32_t* ctx = static_cast<const int32_t*>(d_ctx);
+    (void)d_ids;  // the context carries the ids (as dwords)
+    return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
+                         n_stripes, d_counts ? &in : nullptr, p->sys ? p->k : 0,
+                         nullptr,
+                         reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
+                         cs, p->d_err, st(stream));
 }
 
 int qi_gpu_take_error(qi_plan* p)

@@ -25,6 +25,19 @@ struct MatLayout {
     __host__ __device__ size_t words() const { return plain() + static_cast<size_t>(R) * kin; }
 };
 
+// OOR routing: the decode context keeps, per stripe and per tile of
+// kRouteTile columns, the marks of the received rows that fall in the tile
+// (count + up to kRouteCap entries packed as position << 16 | column-in-tile).
+// A count above kRouteCap makes the decode kernel scan the OOR buckets.
+constexpr int kRouteTile = 512;
+constexpr int kRouteCap = 15;
+constexpr int kRouteStride = kRouteCap + 1;
+
+__host__ __device__ inline long long route_tiles(long long words)
+{
+    return (words + kRouteTile - 1) / kRouteTile;
+}
+
 // Row source for the matrix kernel: fragment `id` of stripe `s` is at
 //   id <  split : base0 + s*ss0 + id*rs0
 //   id >= split : base1 + s*ss1 + (id-split)*rs1        (elements of u16)
@@ -63,21 +76,30 @@ int launch_encode_fnt(int k, int n, int n_out, const int32_t* d_twist,
 
 // out[t] = sum_i M[t][i] * in[ids[i]]  for t < R
 //   mat: per-stripe blocks (mat_stride words apart; 0 = shared)
-//   ids: S x kin fragment ids (nullptr = identity 0..kin-1)
+//   ids: per-stripe kin int32 fragment ids, ids_stride apart (nullptr =
+//   identity 0..kin-1)
 //   in_oor: restore buckets by slot (nullptr = none); slot_of_id = id -
 //     slot_base (ids < slot_base have no bucket)
 //   out_oor: record OOR outputs (nullptr = no recording; values stored as 0)
+//   route: per-stripe OOR routing tables (route_stride u32 apart), or null
 int launch_matrix(const MatLayout& L, const int32_t* mat, long long mat_stride,
-                  const uint16_t* ids, RowSrc src, RowDst dst, long long words,
+                  const int32_t* ids, long long ids_stride, RowSrc src,
+                  RowDst dst, long long words,
                   int n_stripes, const Oor* in_oor, int slot_base,
-                  const Oor* out_oor, uint32_t* d_err, hipStream_t stream);
+                  const Oor* out_oor, const uint32_t* route,
+                  long long route_stride, uint32_t* d_err, hipStream_t stream);
 
 // per-stripe decode matrices from fragment ids (S x k).
 //   mode 0: coefficient extraction (non-systematic: data = poly coefs)
 //   mode 1: evaluation at r^t, t < k (systematic: data = P(r^t))
-int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
-                      const uint16_t* d_ids, int n_stripes, int32_t* d_mat,
-                      hipStream_t stream);
+//   d_ctx: per stripe ctx_stride words: the MatLayout block, the k ids as
+//   int32, then the OOR route table (route_tiles(words) x kRouteStride u32)
+//   built from in_oor
+//   (slot = by_pos ? position : id - slot_base); in_oor may be null.
+int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
+                      const uint16_t* d_ids, int n_stripes, int32_t* d_ctx,
+                      long long ctx_stride, const Oor* in_oor, int slot_base,
+                      int by_pos, long long words, hipStream_t stream);
 
 // matrix kernel instantiation choice
 int matrix_kp(int kin);

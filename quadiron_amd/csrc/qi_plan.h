@@ -57,6 +57,16 @@ struct HostState {
 
 }  // namespace qi
 
+struct qi_plan;
+
+namespace qi {
+// per-stripe decode context stride (int32 words) and builder (qi_gpu.cpp)
+long long ctx_stride(const qi_plan* p, long long words);
+int build_ctx(qi_plan* p, const uint16_t* d_ids, const uint16_t* h_ids,
+              int n_stripes, const Oor* in, int slot_base, int by_pos,
+              long long words, void* d_ctx, hipStream_t s);
+}  // namespace qi
+
 struct qi_plan {
     int k = 0, m = 0, sys = 0, code_len = 0, n_outputs = 0, n = 0, K = 0;
     uint32_t r = 0;

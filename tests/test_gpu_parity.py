@@ -133,8 +133,9 @@ def test_cabi_errors(hip_lib):
 
 # ------------------------------------------- device batch API vs oracle
 
-def _craft(k, m, sys_, data_rows, rng, n_cols):
-    """Force some outputs to 65536 (OOR) by solving for data row 0."""
+def _craft(k, m, sys_, data_rows, rng, n_cols, rows=None, col_range=None):
+    """Force some outputs to 65536 (OOR) by solving for data row 0
+    (optionally only on output `rows`, in columns `col_range`)."""
     o = oracle()
     c = codec(k, m, sys_)
     first = k if sys_ else 0
@@ -152,11 +153,13 @@ def _craft(k, m, sys_, data_rows, rng, n_cols):
 
     a = enc([1] + [0] * (k - 1))
     P = data_rows.shape[1]
-    for j in rng.choice(P, min(n_cols, P), replace=False):
+    lo, hi = col_range if col_range else (0, P)
+    for j in lo + rng.choice(hi - lo, min(n_cols, hi - lo), replace=False):
         col = data_rows[:, j].astype(np.int64)
         col[0] = 0
         b = enc(col)
-        i = int(rng.integers(0, c.n_outputs))
+        i = int(rng.choice(rows)) if rows is not None else int(
+            rng.integers(0, c.n_outputs))
         if a[i] == 0:
             continue
         d0 = ((65536 - b[i]) % Q) * pow(a[i], Q - 2, Q) % Q
@@ -201,8 +204,8 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
     for s in range(S):
         ids[s] = np.sort(rng.choice(k + m, k, replace=False))
     di = torch.from_numpy(ids.view(np.int16)).cuda()
-    ctx = torch.zeros(plan.ctx_bytes(S), dtype=torch.uint8, device="cuda")
-    plan.decode_ctx(di, ctx, h_ids=ids)
+    ctx = torch.zeros(plan.ctx_bytes(S, P), dtype=torch.uint8, device="cuda")
+    plan.decode_ctx(di, ctx, P, counts, entries, cap, h_ids=ids)
     dec = torch.zeros((S, k, P), dtype=torch.int16, device="cuda")
     err = plan.decode(ctx, di, out, dec, data=dd, counts=counts,
                       entries=entries, cap=cap)
@@ -253,3 +256,34 @@ def test_empty_and_tiny_blocks(hip_lib):
         outs, oor, cnt = fec_encode(hip_lib, k, m, 0, data, 64)
         o_out, o_oor, o_cnt = oracle_encode_blocks(k, m, 0, data, 64)
         assert (outs == o_out).all() and (cnt == o_cnt).all()
+
+
+def test_dense_oor_tile_uses_bucket_scan():
+    """More than kRouteCap (15) marks of received rows inside one 512-column
+    tile: the decode falls back from the context's route table to scanning
+    the OOR buckets; output still bit-exact."""
+    torch = _torch()
+    import quadiron_amd as qa
+    k, m, S, P = 16, 48, 1, 2048
+    rng = np.random.default_rng(99)
+    data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
+    _craft(k, m, 0, data[0], rng, 200, rows=range(k), col_range=(512, 1024))
+    plan = qa.Plan(k, m, False)
+    no = plan.n_outputs
+    dd = torch.from_numpy(data.view(np.int16)).cuda()
+    out = torch.zeros((S, no, P), dtype=torch.int16, device="cuda")
+    cap = 512
+    counts = torch.zeros(S * no, dtype=torch.int32, device="cuda")
+    entries = torch.zeros(S * no * cap, dtype=torch.int32, device="cuda")
+    plan.encode(dd, out, counts, entries, cap)
+    ids = np.arange(k, dtype=np.uint16)[None, :]
+    di = torch.from_numpy(ids.view(np.int16)).cuda()
+    ctx = torch.zeros(plan.ctx_bytes(S, P), dtype=torch.uint8, device="cuda")
+    plan.decode_ctx(di, ctx, P, counts, entries, cap)
+    dec = torch.zeros_like(dd)
+    assert plan.decode(ctx, di, out, dec, counts=counts, entries=entries,
+                       cap=cap) == 0
+    torch.cuda.synchronize()
+    cnt = counts.cpu().numpy()[:k]
+    assert cnt.sum() > 100, cnt
+    assert torch.equal(dec, dd)
