@@ -75,21 +75,72 @@ struct Region {
     }
 };
 
+// NDW (1 or 2) dwords per lane of the row at byte offset `row`
+template <int NDW, bool BUF>
+__device__ __forceinline__ void ld_dw(const Region<BUF>& g, uint32_t row,
+                                      uint32_t voff, uint32_t (&w)[NDW])
+{
+    static_assert(NDW == 1 || NDW == 2, "dword count");
+    if constexpr (NDW == 1) {
+        if constexpr (BUF)
+            w[0] = __builtin_amdgcn_raw_buffer_load_b32(
+                g.r, static_cast<int>(voff), static_cast<int>(row), 0);
+        else
+            w[0] = *reinterpret_cast<const uint32_t*>(g.p + row + voff);
+    } else {
+        if constexpr (BUF) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(
+                g.r, static_cast<int>(voff), static_cast<int>(row), 0);
+            w[0] = v[0];
+            w[1] = v[1];
+        } else {
+            const uint2 v = *reinterpret_cast<const uint2*>(g.p + row + voff);
+            w[0] = v.x;
+            w[1] = v.y;
+        }
+    }
+}
+
+template <int NDW, bool BUF>
+__device__ __forceinline__ void st_dw(const Region<BUF>& g, uint32_t row,
+                                      uint32_t voff, const uint32_t (&w)[NDW])
+{
+    static_assert(NDW == 1 || NDW == 2, "dword count");
+    if constexpr (NDW == 1) {
+        if constexpr (BUF)
+            __builtin_amdgcn_raw_buffer_store_b32(w[0], g.r, static_cast<int>(voff),
+                                                  static_cast<int>(row), 0);
+        else
+            *reinterpret_cast<uint32_t*>(g.p + row + voff) = w[0];
+    } else {
+        if constexpr (BUF) {
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            u32x2 v;
+            v[0] = w[0];
+            v[1] = w[1];
+            __builtin_amdgcn_raw_buffer_store_b64(v, g.r, static_cast<int>(voff),
+                                                  static_cast<int>(row), 0);
+        } else {
+            *reinterpret_cast<uint2*>(g.p + row + voff) = make_uint2(w[0], w[1]);
+        }
+    }
+}
+
 // COLS adjacent u16 columns of the row at byte offset `row` (wave-uniform).
-// FULL: one dword per lane (COLS 2); otherwise columns past `avail` are 0.
+// FULL: COLS/2 dwords per lane (COLS 2 or 4); otherwise one u16 per column
+// and columns past `avail` are 0.
 template <int COLS, bool FULL, bool BUF>
 __device__ __forceinline__ void ld(const Region<BUF>& g, uint32_t row,
                                    uint32_t voff, long long avail, int32_t* v)
 {
-    if constexpr (FULL && COLS == 2) {
-        uint32_t w;
-        if constexpr (BUF)
-            w = __builtin_amdgcn_raw_buffer_load_b32(g.r, static_cast<int>(voff),
-                                                     static_cast<int>(row), 0);
-        else
-            w = *reinterpret_cast<const uint32_t*>(g.p + row + voff);
-        v[0] = w & 0xffff;
-        v[1] = w >> 16;
+    if constexpr (FULL && COLS % 2 == 0) {
+        uint32_t w[COLS / 2];
+        ld_dw<COLS / 2, BUF>(g, row, voff, w);
+#pragma unroll
+        for (int d = 0; d < COLS / 2; d++) {
+            v[2 * d] = w[d] & 0xffff;
+            v[2 * d + 1] = w[d] >> 16;
+        }
     } else {
 #pragma unroll
         for (int c = 0; c < COLS; c++) {
@@ -113,13 +164,12 @@ __device__ __forceinline__ void st(const Region<BUF>& g, uint32_t row,
                                    uint32_t voff, long long avail,
                                    const uint32_t* v)
 {
-    if constexpr (FULL && COLS == 2) {
-        const uint32_t w = pack_lo(v[0], v[1]);
-        if constexpr (BUF)
-            __builtin_amdgcn_raw_buffer_store_b32(w, g.r, static_cast<int>(voff),
-                                                  static_cast<int>(row), 0);
-        else
-            *reinterpret_cast<uint32_t*>(g.p + row + voff) = w;
+    if constexpr (FULL && COLS % 2 == 0) {
+        uint32_t w[COLS / 2];
+#pragma unroll
+        for (int d = 0; d < COLS / 2; d++)
+            w[d] = pack_lo(v[2 * d], v[2 * d + 1]);
+        st_dw<COLS / 2, BUF>(g, row, voff, w);
     } else {
 #pragma unroll
         for (int c = 0; c < COLS; c++) {
@@ -288,42 +338,55 @@ struct MatExt {
 };
 
 template <int KP, int COLS, bool FULL, bool BUF>
-__device__ __forceinline__ void matrix_load(int kin, const int (&idv)[2 * KP],
+__device__ __forceinline__ void matrix_load(const int (&idv)[2 * KP],
                                             const RowSrc& src,
                                             const Region<BUF>& g0,
                                             const Region<BUF>& g1, uint32_t voff,
                                             long long avail,
                                             int32_t (&xp)[COLS][KP])
 {
-    // every received row, branch-free (rows past kin are masked to 0), then
-    // offset to signed 16 bit (x - 32768) and pack row pairs for dot2
+    // every row pair, branch-free, offset to signed 16 bit (x - 32768) and
+    // packed [row 2j, row 2j+1] per column for dot2.  Rows past kin load a
+    // valid (clamped) row and need no masking: their packed coefficients are
+    // 0 and kcorr sums only the real ones (pack_row).
 #pragma unroll
     for (int j = 0; j < KP; j++) {
-        int32_t vv[2][COLS];
+        Region<BUF> g[2] = {g0, g0};
+        uint32_t off[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-            const int i = 2 * j + h;
-            const int id = src.by_pos ? (i < kin ? i : kin - 1) : idv[i];
+            const int id = idv[2 * j + h];
             // branch-free source select (uniform s_cselect): a branch here
             // makes the compiler drain vmcnt after every row load
             const bool lo = id < src.split;
-            Region<BUF> g = g0;
             if constexpr (BUF)
-                g.r = lo ? g0.r : g1.r;
-            g.p = lo ? g0.p : g1.p;
-            const uint32_t off = static_cast<uint32_t>(
-                lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
-            ld<COLS, FULL, BUF>(g, off, voff, avail, vv[h]);
+                g[h].r = lo ? g0.r : g1.r;
+            g[h].p = lo ? g0.p : g1.p;
+            off[h] = static_cast<uint32_t>(lo ? id * src.rs0 * 2
+                                              : (id - src.split) * src.rs1 * 2);
+        }
+        if constexpr (FULL && COLS % 2 == 0) {
+            uint32_t w0[COLS / 2], w1[COLS / 2];
+            ld_dw<COLS / 2, BUF>(g[0], off[0], voff, w0);
+            ld_dw<COLS / 2, BUF>(g[1], off[1], voff, w1);
+#pragma unroll
+            for (int d = 0; d < COLS / 2; d++) {
+                xp[2 * d][j] = static_cast<int32_t>(
+                    __builtin_amdgcn_perm(w1[d], w0[d], 0x05040100u) ^ 0x80008000u);
+                xp[2 * d + 1][j] = static_cast<int32_t>(
+                    __builtin_amdgcn_perm(w1[d], w0[d], 0x07060302u) ^ 0x80008000u);
+            }
+        } else {
+            int32_t vv[2][COLS];
+            ld<COLS, FULL, BUF>(g[0], off[0], voff, avail, vv[0]);
+            ld<COLS, FULL, BUF>(g[1], off[1], voff, avail, vv[1]);
 #pragma unroll
             for (int c = 0; c < COLS; c++)
-                vv[h][c] = i < kin ? vv[h][c] : 0;
+                xp[c][j] = static_cast<int32_t>(
+                    pack_lo(static_cast<uint32_t>(vv[0][c]),
+                            static_cast<uint32_t>(vv[1][c])) ^
+                    0x80008000u);
         }
-#pragma unroll
-        for (int c = 0; c < COLS; c++)
-            xp[c][j] = static_cast<int32_t>(
-                pack_lo(static_cast<uint32_t>(vv[0][c]),
-                        static_cast<uint32_t>(vv[1][c])) ^
-                0x80008000u);
     }
 }
 
@@ -469,13 +532,17 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
             idv[i] = i;
     }
 #pragma unroll
-    for (int i = 0; i < 2 * KP; i++)  // clamp rows past kin (masked later)
-        idv[i] = i < kin ? idv[i] : idv[0];
+    for (int i = 0; i < 2 * KP; i++) {
+        // source row of input i: its position (by_pos) or its fragment id;
+        // rows past kin are clamped to a valid row (their coefficients are 0)
+        const int ii = i < kin ? i : kin - 1;
+        idv[i] = src.by_pos ? ii : (i < kin ? idv[i] : idv[0]);
+    }
     int32_t xp[COLS][KP];
     if (full) {
-        matrix_load<KP, COLS, true, BUF>(kin, idv, src, g0, g1, voff, COLS, xp);
+        matrix_load<KP, COLS, true, BUF>(idv, src, g0, g1, voff, COLS, xp);
     } else if (col < words) {
-        matrix_load<KP, COLS, false, BUF>(kin, idv, src, g0, g1, voff,
+        matrix_load<KP, COLS, false, BUF>(idv, src, g0, g1, voff,
                                           words - col, xp);
     }
     int n_lm = 0;
@@ -768,6 +835,35 @@ static int mat_launch(const MatLayout& L, const int32_t* mat, long long ms,
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// columns per lane: 4 (b64 row loads) while the packed rows fit in
+// registers, 2 up to KP 16, else 1; cols 1 is also the flat (BUF=false) path
+template <int KP>
+static int mat_dispatch(int cols, const MatLayout& L, const int32_t* mat,
+                        long long ms, const int32_t* ids, long long is,
+                        RowSrc src, RowDst dst, MatExt ext, long long words,
+                        int S, Oor io, int slot_base, Oor oo,
+                        const uint32_t* route, long long rstride, uint32_t* err,
+                        hipStream_t st)
+{
+    const bool buf = ext.e0 && ext.eo && (!src.base1 || ext.e1);
+    if (!buf)
+        return mat_launch<KP, 1, false>(L, mat, ms, ids, is, src, dst, ext,
+                                        words, S, io, slot_base, oo, route,
+                                        rstride, err, st);
+    if constexpr (KP <= 8)
+        if (cols == 4)
+            return mat_launch<KP, 4, true>(L, mat, ms, ids, is, src, dst, ext,
+                                           words, S, io, slot_base, oo, route,
+                                           rstride, err, st);
+    if constexpr (KP <= 16)
+        if (cols >= 2)
+            return mat_launch<KP, 2, true>(L, mat, ms, ids, is, src, dst, ext,
+                                           words, S, io, slot_base, oo, route,
+                                           rstride, err, st);
+    return mat_launch<KP, 1, true>(L, mat, ms, ids, is, src, dst, ext, words, S,
+                                   io, slot_base, oo, route, rstride, err, st);
+}
+
 int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
                   const int32_t* ids, long long is, RowSrc src, RowDst dst,
                   long long words,
@@ -788,28 +884,34 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
                extent(src.rows1, src.rs1, words),
                extent(L.R, dst.rs, words)};
     const bool buf = ext.e0 && ext.eo && (!src.base1 || ext.e1);
-#define QI_MAT(KK)                                                             \
-    if (L.KP == KK) {                                                          \
-        if (!buf)                                                              \
-            return mat_launch<KK, 1, false>(L, mat, ms, ids, is, src, dst, ext,     \
-                                            words, S, io, slot_base, oo,       \
-                                            route, rstride, err, st);          \
-        return (a2 && KK <= 16)                                                \
-                   ? mat_launch<KK, 2, true>(L, mat, ms, ids, is, src, dst, ext,   \
-                                             words, S, io, slot_base, oo,      \
-                                             route, rstride, err, st)          \
-                   : mat_launch<KK, 1, true>(L, mat, ms, ids, is, src, dst, ext,   \
-                                             words, S, io, slot_base, oo,      \
-                                             route, rstride, err, st);         \
+    const bool a4 = a2 &&
+                    aligned_for(4, src.base0, src.ss0, src.rs0, dst.ss, dst.rs) &&
+                    (src.base1 == nullptr ||
+                     aligned_for(4, src.base1, src.ss1, src.rs1, 0, 0)) &&
+                    (reinterpret_cast<uintptr_t>(dst.base) % 8) == 0;
+    const int cols = !buf ? 1 : a4 ? 4 : a2 ? 2 : 1;
+    switch (L.KP) {
+    case 2:
+        return mat_dispatch<2>(cols, L, mat, ms, ids, is, src, dst, ext, words,
+                               S, io, slot_base, oo, route, rstride, err, st);
+    case 4:
+        return mat_dispatch<4>(cols, L, mat, ms, ids, is, src, dst, ext, words,
+                               S, io, slot_base, oo, route, rstride, err, st);
+    case 8:
+        return mat_dispatch<8>(cols, L, mat, ms, ids, is, src, dst, ext, words,
+                               S, io, slot_base, oo, route, rstride, err, st);
+    case 16:
+        return mat_dispatch<16>(cols, L, mat, ms, ids, is, src, dst, ext, words,
+                                S, io, slot_base, oo, route, rstride, err, st);
+    case 32:
+        return mat_dispatch<32>(cols, L, mat, ms, ids, is, src, dst, ext, words,
+                                S, io, slot_base, oo, route, rstride, err, st);
+    case 64:
+        return mat_dispatch<64>(cols, L, mat, ms, ids, is, src, dst, ext, words,
+                                S, io, slot_base, oo, route, rstride, err, st);
+    default:
+        return -3;
     }
-    QI_MAT(2)
-    QI_MAT(4)
-    QI_MAT(8)
-    QI_MAT(16)
-    QI_MAT(32)
-    QI_MAT(64)
-#undef QI_MAT
-    return -3;
 }
 
 int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,

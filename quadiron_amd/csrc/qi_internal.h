@@ -29,7 +29,7 @@ struct MatLayout {
 // kRouteTile columns, the marks of the received rows that fall in the tile
 // (count + up to kRouteCap entries packed as position << 16 | column-in-tile).
 // A count above kRouteCap makes the decode kernel scan the OOR buckets.
-constexpr int kRouteTile = 512;
+constexpr int kRouteTile = 1024;  // a multiple of every block width (256*COLS)
 constexpr int kRouteCap = 15;
 constexpr int kRouteStride = kRouteCap + 1;
 

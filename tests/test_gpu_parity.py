@@ -259,7 +259,7 @@ def test_empty_and_tiny_blocks(hip_lib):
 
 
 def test_dense_oor_tile_uses_bucket_scan():
-    """More than kRouteCap (15) marks of received rows inside one 512-column
+    """More than kRouteCap (15) marks of received rows inside one 1024-column
     tile: the decode falls back from the context's route table to scanning
     the OOR buckets; output still bit-exact."""
     torch = _torch()
