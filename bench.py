@@ -127,7 +127,7 @@ def main():
             e1.record()
         plan.decode_ctx(ids, ctx, P, counts, entries, cap, stream=stream)
         plan.decode(ctx, ids, coded, dec, counts=counts, entries=entries,
-                    cap=cap, stream=stream)
+                    cap=cap, stream=stream, check=False)
         if timed:
             e2.record()
             ev.append((e0, e1, e2))
@@ -136,7 +136,7 @@ def main():
         step(False)
     torch.cuda.synchronize()
     # correctness of the measured pipeline (outside the timed region)
-    ok = bool(torch.equal(dec, data))
+    ok = bool(torch.equal(dec, data)) and plan.take_error() == 0
     oor_max = int(counts.max().item())
     if dist:
         dist.barrier()
@@ -148,6 +148,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ok = ok and plan.take_error() == 0
     if dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

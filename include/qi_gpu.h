@@ -94,6 +94,25 @@ int qi_gpu_decode(qi_plan* plan, const void* d_ctx, const uint16_t* d_ids,
                   long long out_row_stride, long long words, int n_stripes,
                   void* stream);
 
+/* Packed-row decode (the staging layout of a host pipeline, where the k
+ * received fragments of a stripe are copied back to back): row i of stripe s
+ * is read from d_recv + s*rss + i*rrs and holds fragment d_ids[s*k + i].  The
+ * OOR buckets are indexed by that position i (slots = k).  Contexts for this
+ * layout come from qi_gpu_decode_ctx_packed (same size as
+ * qi_gpu_decode_ctx_bytes). */
+int qi_gpu_decode_ctx_packed(qi_plan* plan, const uint16_t* d_ids,
+                             const uint16_t* h_ids, int n_stripes,
+                             const uint32_t* d_oor_counts,
+                             const uint32_t* d_oor_entries, int oor_cap,
+                             long long words, void* d_ctx, void* stream);
+int qi_gpu_decode_packed(qi_plan* plan, const void* d_ctx,
+                         const uint16_t* d_recv, long long rss, long long rrs,
+                         const uint32_t* d_oor_counts,
+                         const uint32_t* d_oor_entries, int oor_cap,
+                         uint16_t* d_out, long long out_stripe_stride,
+                         long long out_row_stride, long long words,
+                         int n_stripes, void* stream);
+
 /* Non-zero if a decode overflowed its per-tile OOR scratch (sticky; reset
  * by reading). Synchronous. */
 int qi_gpu_take_error(qi_plan* plan);

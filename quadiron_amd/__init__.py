@@ -48,6 +48,9 @@ def _declare(lib):
         "qi_gpu_decode_ctx": (I, [V, V, V, I, V, V, I, LL, V, V]),
         "qi_gpu_decode": (I, [V, V, V, V, LL, LL, V, LL, LL, V, V, I, V, LL,
                               LL, LL, I, V]),
+        "qi_gpu_decode_ctx_packed": (I, [V, V, V, I, V, V, I, LL, V, V]),
+        "qi_gpu_decode_packed": (I, [V, V, V, LL, LL, V, V, I, V, LL, LL, LL,
+                                     I, V]),
         "qi_gpu_take_error": (I, [V]),
         "qi_fec_new": (V, [I, I, I]),
         "qi_fec_delete": (None, [V]),
@@ -156,8 +159,11 @@ class Plan:
             raise RuntimeError(f"qi_gpu_decode_ctx failed: {rc}")
 
     def decode(self, ctx, ids, coded, out, data=None, counts=None,
-               entries=None, cap=0, stream=None):
-        """coded: [S, n_out, P] (fragment slot rows); out: [S, k, P]."""
+               entries=None, cap=0, stream=None, check=True):
+        """coded: [S, n_out, P] (fragment slot rows); out: [S, k, P].
+        check: synchronise and return the sticky OOR-overflow flag
+        (qi_gpu_take_error); with check=False the call stays asynchronous
+        and returns 0 -- call take_error() later."""
         S, _, P = out.shape
         d = data if data is not None else coded
         rc = lib().qi_gpu_decode(
@@ -169,6 +175,38 @@ class Plan:
             self._stream(stream))
         if rc:
             raise RuntimeError(f"qi_gpu_decode failed: {rc}")
+        return lib().qi_gpu_take_error(self.h) if check else 0
+
+    def decode_ctx_packed(self, ids, ctx, words, counts=None, entries=None,
+                          cap=0, h_ids=None, stream=None):
+        """Contexts for decode_packed: OOR buckets indexed by the position
+        of the received row (slots = k)."""
+        rc = lib().qi_gpu_decode_ctx_packed(
+            self.h, ids.data_ptr(),
+            h_ids.ctypes.data_as(C.c_void_p) if h_ids is not None else None,
+            ids.shape[0],
+            counts.data_ptr() if counts is not None else None,
+            entries.data_ptr() if entries is not None else None, int(cap),
+            words, ctx.data_ptr(), self._stream(stream))
+        if rc:
+            raise RuntimeError(f"qi_gpu_decode_ctx_packed failed: {rc}")
+
+    def decode_packed(self, ctx, recv, out, counts=None, entries=None, cap=0,
+                      stream=None, check=True):
+        """recv: [S, k, P] received rows in id order; out: [S, k, P]."""
+        S, _, P = out.shape
+        rc = lib().qi_gpu_decode_packed(
+            self.h, ctx.data_ptr(), recv.data_ptr(), recv.stride(0),
+            recv.stride(1),
+            counts.data_ptr() if counts is not None else None,
+            entries.data_ptr() if entries is not None else None, int(cap),
+            out.data_ptr(), out.stride(0), out.stride(1), P, S,
+            self._stream(stream))
+        if rc:
+            raise RuntimeError(f"qi_gpu_decode_packed failed: {rc}")
+        return lib().qi_gpu_take_error(self.h) if check else 0
+
+    def take_error(self):
         return lib().qi_gpu_take_error(self.h)
 
 

@@ -166,6 +166,42 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
                          cs, p->d_err, st(stream));
 }
 
+int qi_gpu_decode_ctx_packed(qi_plan* p, const uint16_t* d_ids,
+                             const uint16_t* h_ids, int n_stripes,
+                             const uint32_t* d_counts, const uint32_t* d_entries,
+                             int cap, long long words, void* d_ctx, void* stream)
+{
+    if (!p || !d_ctx || n_stripes < 0 || words < 0)
+        return -1;
+    Oor in{const_cast<uint32_t*>(d_counts), const_cast<uint32_t*>(d_entries),
+           p->k, cap};
+    return qi::build_ctx(p, d_ids, h_ids, n_stripes, d_counts ? &in : nullptr, 0,
+                         1, words, d_ctx, st(stream));
+}
+
+int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
+                         long long rss, long long rrs, const uint32_t* d_counts,
+                         const uint32_t* d_entries, int cap, uint16_t* d_out,
+                         long long oss, long long ors, long long words,
+                         int n_stripes, void* stream)
+{
+    if (!p || !d_ctx || !d_recv || !d_out || n_stripes < 0 || words < 0)
+        return -1;
+    if (n_stripes == 0 || words == 0)
+        return 0;
+    const MatLayout L = ctx_layout(p);
+    RowSrc src{d_recv, rss, rrs, 1 << 30, nullptr, 0, 0, 1, p->k, 0};
+    Oor in{const_cast<uint32_t*>(d_counts), const_cast<uint32_t*>(d_entries),
+           p->k, cap};
+    RowDst out{d_out, oss, ors};
+    const long long cs = ctx_stride(p, words);
+    const int32_t* ctx = static_cast<const int32_t*>(d_ctx);
+    return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
+                         n_stripes, d_counts ? &in : nullptr, 0, nullptr,
+                         reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
+                         cs, p->d_err, st(stream));
+}
+
 int qi_gpu_take_error(qi_plan* p)
 {
     if (!p)

@@ -212,6 +212,28 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
     torch.cuda.synchronize()
     assert err == 0
     assert (dec.cpu().numpy().view(np.uint16) == data).all()
+
+    # the packed staging layout (qi_gpu_decode_packed): received rows back
+    # to back in id order, OOR buckets by position
+    idx = torch.from_numpy(ids.astype(np.int64)).cuda()
+    if sys_:
+        full = torch.cat([dd, out], dim=1)
+        zc = torch.zeros((S, k), dtype=torch.int32, device="cuda")
+        fcnt = torch.cat([zc, counts.view(S, no)], dim=1)
+        fent = torch.cat([torch.zeros((S, k, cap), dtype=torch.int32,
+                                      device="cuda"),
+                          entries.view(S, no, cap)], dim=1)
+    else:
+        full, fcnt, fent = out, counts.view(S, no), entries.view(S, no, cap)
+    recv = torch.gather(full, 1, idx[:, :, None].expand(S, k, P)).contiguous()
+    pcnt = torch.gather(fcnt, 1, idx).contiguous()
+    pent = torch.gather(fent, 1, idx[:, :, None].expand(S, k, cap)).contiguous()
+    ctx2 = torch.zeros_like(ctx)
+    plan.decode_ctx_packed(di, ctx2, P, pcnt, pent, cap, h_ids=ids)
+    dec2 = torch.zeros_like(dec)
+    assert plan.decode_packed(ctx2, recv, dec2, pcnt, pent, cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec2, dd)
     return plan
 
 

@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Host-inclusive RS-FNT rate (DESIGN.md "Host-inclusive rate").
+
+The path starts and ends in host memory (shard files / socket buffers).  This
+measures cfg2 (k=16, n=64, 64 KiB packets) with every byte crossing PCIe:
+
+  encode:  pinned data rows --H2D--> encode --D2H--> pinned coded rows
+  decode:  pinned received rows (k per stripe, packed in id order) --H2D-->
+           decode_ctx_packed + decode_packed --D2H--> pinned data rows
+
+in chunks of C stripes round-robin over 3 HIP streams (copy / compute
+overlap), plus the raw pinned H2D / D2H copy rates.  Rates use the same
+algorithmic bytes as bench.py: encode (k+n)*2P, decode 2k*2P per stripe.
+
+    python tools/host_rate.py [--stripes 512] [--chunk 32]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import quadiron_amd as qa  # noqa: E402
+from bench import alg_bytes  # noqa: E402
+
+
+def copy_rate(nbytes, h2d):
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    for _ in range(2):
+        (d.copy_(h, non_blocking=True) if h2d else h.copy_(d, non_blocking=True))
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(5):
+        (d.copy_(h, non_blocking=True) if h2d else h.copy_(d, non_blocking=True))
+    torch.cuda.synchronize()
+    return 5 * nbytes / (time.perf_counter() - t) / 1e9
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stripes", type=int, default=512)
+    ap.add_argument("--chunk", type=int, default=32)
+    ap.add_argument("--streams", type=int, default=3)
+    args = ap.parse_args()
+    k, m, P = 16, 48, 32768
+    S, Cn, NS = args.stripes, args.chunk, args.streams
+    assert S % Cn == 0
+    plan = qa.Plan(k, m, False)
+    n = plan.n_outputs
+    cap = 64
+    rng = np.random.default_rng(7)
+
+    h_data = torch.from_numpy(
+        rng.integers(-32768, 32768, (S, k, P), dtype=np.int16)).pin_memory()
+    h_coded = torch.empty((S, n, P), dtype=torch.int16, pin_memory=True)
+    h_cnt = torch.empty((S, n), dtype=torch.int32, pin_memory=True)
+    h_ent = torch.empty((S, n, cap), dtype=torch.int32, pin_memory=True)
+    h_dec = torch.empty((S, k, P), dtype=torch.int16, pin_memory=True)
+    streams = [torch.cuda.Stream() for _ in range(NS)]
+    dev = [dict(data=torch.empty((Cn, k, P), dtype=torch.int16, device="cuda"),
+                coded=torch.empty((Cn, n, P), dtype=torch.int16, device="cuda"),
+                dec=torch.empty((Cn, k, P), dtype=torch.int16, device="cuda"),
+                cnt=torch.empty((Cn, n), dtype=torch.int32, device="cuda"),
+                ent=torch.empty((Cn, n, cap), dtype=torch.int32, device="cuda"),
+                ids=torch.empty((Cn, k), dtype=torch.int16, device="cuda"),
+                pcnt=torch.empty((Cn, k), dtype=torch.int32, device="cuda"),
+                pent=torch.empty((Cn, k, cap), dtype=torch.int32, device="cuda"),
+                ctx=torch.empty(plan.ctx_bytes(Cn, P), dtype=torch.uint8,
+                                device="cuda"))
+           for _ in range(NS)]
+
+    def encode_all():
+        for c in range(S // Cn):
+            b, st = dev[c % NS], streams[c % NS]
+            sl = slice(c * Cn, (c + 1) * Cn)
+            with torch.cuda.stream(st):
+                b["data"].copy_(h_data[sl], non_blocking=True)
+                b["cnt"].zero_()
+                plan.encode(b["data"], b["coded"], b["cnt"], b["ent"], cap,
+                            stream=st.cuda_stream)
+                h_coded[sl].copy_(b["coded"], non_blocking=True)
+                h_cnt[sl].copy_(b["cnt"], non_blocking=True)
+                h_ent[sl].copy_(b["ent"], non_blocking=True)
+        torch.cuda.synchronize()
+
+    encode_all()  # warm-up
+    t0 = time.perf_counter()
+    encode_all()
+    t_enc = time.perf_counter() - t0
+
+    # received fragments: a random k-subset per stripe, staged back to back
+    # (what the network / file reader would deliver), not timed
+    ids = np.sort(np.stack([rng.choice(k + m, k, replace=False)
+                            for _ in range(S)]), axis=1)
+    idx = torch.from_numpy(ids.astype(np.int64))
+    h_recv = torch.gather(h_coded, 1, idx[:, :, None].expand(S, k, P)).pin_memory()
+    h_pcnt = torch.gather(h_cnt, 1, idx).pin_memory()
+    h_pent = torch.gather(h_ent, 1, idx[:, :, None].expand(S, k, cap)).pin_memory()
+    h_ids = torch.from_numpy(ids.astype(np.int16)).pin_memory()
+
+    def decode_all():
+        for c in range(S // Cn):
+            b, st = dev[c % NS], streams[c % NS]
+            sl = slice(c * Cn, (c + 1) * Cn)
+            with torch.cuda.stream(st):
+                b["data"].copy_(h_recv[sl], non_blocking=True)
+                b["ids"].copy_(h_ids[sl], non_blocking=True)
+                b["pcnt"].copy_(h_pcnt[sl], non_blocking=True)
+                b["pent"].copy_(h_pent[sl], non_blocking=True)
+                plan.decode_ctx_packed(b["ids"], b["ctx"], P, b["pcnt"],
+                                       b["pent"], cap, stream=st.cuda_stream)
+                plan.decode_packed(b["ctx"], b["data"], b["dec"],
+                                   b["pcnt"], b["pent"], cap,
+                                   stream=st.cuda_stream, check=False)
+                h_dec[sl].copy_(b["dec"], non_blocking=True)
+        torch.cuda.synchronize()
+
+    decode_all()
+    t0 = time.perf_counter()
+    decode_all()
+    t_dec = time.perf_counter() - t0
+    ok = bool(torch.equal(h_dec, h_data)) and plan.take_error() == 0
+
+    enc_b, dec_b = alg_bytes(k, m, P)
+    out = {
+        "what": "host-inclusive RS-FNT k=16 n=64 pkt=64KiB (pinned host "
+                "buffers, H2D + kernels + D2H, chunked over streams)",
+        "stripes": S, "chunk_stripes": Cn, "streams": NS,
+        "h2d_GBps": copy_rate(256 << 20, True),
+        "d2h_GBps": copy_rate(256 << 20, False),
+        "encode_ms_per_stripe": t_enc / S * 1e3,
+        "decode_ms_per_stripe": t_dec / S * 1e3,
+        "encode_GBps": S * enc_b / t_enc / 1e9,
+        "decode_GBps": S * dec_b / t_dec / 1e9,
+        "encdec_GBps": S * (enc_b + dec_b) / (t_enc + t_dec) / 1e9,
+        "pcie_bytes_per_stripe": {"h2d": (k + k) * 2 * P,
+                                  "d2h": (n + k) * 2 * P},
+        "roundtrip_ok": ok,
+    }
+    print(json.dumps(out))
+    return 0 if ok else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main())
