@@ -71,6 +71,28 @@ def cpu_baseline(k, m, P, threads, stripes_per_thread):
     return None
 
 
+def shard(rank, world, stripes_per_gpu):
+    """Global stripe range [lo, hi) of a rank: the batch partitions by stripe
+    (independent codewords), weak scaling -- no data-path collective."""
+    return rank * stripes_per_gpu, (rank + 1) * stripes_per_gpu
+
+
+def reduce_over_ranks(dist, elapsed, ok, device):
+    """MAX of the per-rank timed-region wall time and AND of the per-rank
+    round-trip checks (the only collectives in the bench)."""
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    okt = torch.tensor([1 if ok else 0], device=device, dtype=torch.int32)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    return t.item(), bool(okt.item())
+
+
+def aggregate_value(world, stripes_per_gpu, steps, k, m, P, elapsed):
+    """Whole-job GB/s: algorithmic bytes of every rank's stripes / max time."""
+    enc_b, dec_b = alg_bytes(k, m, P)
+    return world * stripes_per_gpu * steps * (enc_b + dec_b) / elapsed / 1e9
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,7 +122,8 @@ def main():
     n_out = plan.n_outputs
     cap = 64
     g = torch.Generator(device=dev)
-    g.manual_seed(0x51D00001 + rank)
+    lo, _ = shard(rank, world, S)
+    g.manual_seed(0x51D00001 + lo)  # this rank's shard of the global batch
     data = torch.randint(-32768, 32768, (S, k, P), dtype=torch.int16,
                          device=dev, generator=g)
     coded = torch.empty((S, n_out, P), dtype=torch.int16, device=dev)
@@ -150,16 +173,10 @@ def main():
     elapsed = time.perf_counter() - t0
     ok = ok and plan.take_error() == 0
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-        okt = torch.tensor([1 if ok else 0], device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
+        elapsed, ok = reduce_over_ranks(dist, elapsed, ok, dev)
 
     enc_b, dec_b = alg_bytes(k, m, P)
-    total_bytes = world * S * args.steps * (enc_b + dec_b)
-    value = total_bytes / elapsed / 1e9
+    value = aggregate_value(world, S, args.steps, k, m, P, elapsed)
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     enc_gbs = S * enc_b / (enc_ms * 1e-3) / 1e9

@@ -296,7 +296,10 @@ __device__ __forceinline__ void encode_body(
 }
 
 template <int K, int COLS, bool KEQ, bool BUF>
-__global__ __launch_bounds__(kBlock) void encode_fnt_kernel(
+// 4 waves per SIMD: the K=16, COLS=2 body fits 128 VGPRs without spills or
+// extra instructions (3 waves at the compiler's default 130)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void
+encode_fnt_kernel(
     int k, int n, int n_out, const int32_t* __restrict__ twist,
     const uint16_t* __restrict__ data, long long dss, uint32_t irs,
     uint32_t iext, uint16_t* __restrict__ out, long long oss, uint32_t ors,
