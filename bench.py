@@ -28,19 +28,27 @@ sys.path.insert(0, ROOT)
 import quadiron_amd as qa  # noqa: E402
 
 K_DATA, M_PAR, PKT_BYTES = 16, 48, 65536
+# BASELINE.json configs measurable on one GPU: (k, m, packet bytes, stripes).
+# cfg2 is the headline metric (the default); the others are extra lines.
+CONFIGS = {
+    "cfg2": (16, 48, 65536, 4096),
+    "cfg3": (64, 960, 4096, 1024),   # high fragmentation, n = 1024
+    "cfg1": (4, 4, 1024, 100),       # the reference's CPU plumbing case
+}
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 
 
-def alg_bytes(k, m, P):
-    """Algorithmic HBM bytes per stripe:
-    encode (k + n) * 2P, decode (k + k) * 2P."""
+def alg_bytes(k, m, P, systematic=False):
+    """Algorithmic HBM bytes per stripe: encode (k + n) * 2P
+    (systematic: (k + m) * 2P), decode (k + k) * 2P."""
     n = 1
     while n < k + m:
         n *= 2
-    return (k + n) * 2 * P, 2 * k * 2 * P
+    enc_rows = k + (m if systematic else n)
+    return enc_rows * 2 * P, 2 * k * 2 * P
 
 
-def cpu_baseline(k, m, P, threads, stripes_per_thread):
+def cpu_baseline(k, m, P, threads, stripes_per_thread, systematic=False):
     """QuadIron's own AVX2 path (oracle/_ref/libqiref_avx2.so, compiled from
     the reference sources) timed on this host: `threads` independent replicas
     (the reference bench's -g model) each encoding + decoding
@@ -49,7 +57,7 @@ def cpu_baseline(k, m, P, threads, stripes_per_thread):
     is absent."""
     import ctypes as C
     ref = os.path.join(ROOT, "oracle", "_ref", "libqiref_avx2.so")
-    enc_b, dec_b = alg_bytes(k, m, P)
+    enc_b, dec_b = alg_bytes(k, m, P, systematic)
     if os.path.exists(ref):
         lib = C.CDLL(ref)
         lib.ref_bench.restype = C.c_double
@@ -58,14 +66,15 @@ def cpu_baseline(k, m, P, threads, stripes_per_thread):
         missing[rng.choice(k + m, m, replace=False)] = 1
         e = C.c_double()
         d = C.c_double()
-        wall = lib.ref_bench(0, k, m, C.c_size_t(P), stripes_per_thread,
+        wall = lib.ref_bench(int(systematic), k, m, C.c_size_t(P), stripes_per_thread,
                              threads, missing.ctypes.data_as(C.c_void_p),
                              C.byref(e), C.byref(d))
         total = threads * stripes_per_thread * (enc_b + dec_b)
         return {"value": total / wall / 1e9, "unit": "GB/s", "cores": threads,
                 "kind": "reference",
                 "sample": f"{threads} threads x {stripes_per_thread} stripes "
-                          f"of RS-FNT k={k} n=64 pkt=64KiB enc+dec "
+                          f"of RS-FNT{'-sys' if systematic else ''} k={k} "
+                          f"m={m} pkt={2 * P // 1024}KiB enc+dec "
                           f"(QuadIron AVX2 build, pkt_size {P} words), "
                           f"wall {wall:.2f}s"}
     return None
@@ -87,9 +96,10 @@ def reduce_over_ranks(dist, elapsed, ok, device):
     return t.item(), bool(okt.item())
 
 
-def aggregate_value(world, stripes_per_gpu, steps, k, m, P, elapsed):
+def aggregate_value(world, stripes_per_gpu, steps, k, m, P, elapsed,
+                    systematic=False):
     """Whole-job GB/s: algorithmic bytes of every rank's stripes / max time."""
-    enc_b, dec_b = alg_bytes(k, m, P)
+    enc_b, dec_b = alg_bytes(k, m, P, systematic)
     return world * stripes_per_gpu * steps * (enc_b + dec_b) / elapsed / 1e9
 
 
@@ -98,7 +108,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--stripes", type=int, default=4096)
+    ap.add_argument("--stripes", type=int, default=None)
+    ap.add_argument("--cfg", choices=sorted(CONFIGS), default="cfg2")
+    ap.add_argument("--systematic", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-stripes", type=int, default=200)
@@ -116,9 +128,13 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    k, m, S = K_DATA, M_PAR, args.stripes
-    P = PKT_BYTES // 2
-    plan = qa.Plan(k, m, False)
+    k, m, pkt_bytes, S = CONFIGS[args.cfg]
+    if args.stripes:
+        S = args.stripes
+    P = pkt_bytes // 2
+    sys_ = bool(args.systematic)
+    headline = args.cfg == "cfg2" and not sys_
+    plan = qa.Plan(k, m, sys_)
     n_out = plan.n_outputs
     cap = 64
     g = torch.Generator(device=dev)
@@ -149,8 +165,8 @@ def main():
         if timed:
             e1.record()
         plan.decode_ctx(ids, ctx, P, counts, entries, cap, stream=stream)
-        plan.decode(ctx, ids, coded, dec, counts=counts, entries=entries,
-                    cap=cap, stream=stream, check=False)
+        plan.decode(ctx, ids, coded, dec, data=data, counts=counts,
+                    entries=entries, cap=cap, stream=stream, check=False)
         if timed:
             e2.record()
             ev.append((e0, e1, e2))
@@ -175,8 +191,8 @@ def main():
     if dist:
         elapsed, ok = reduce_over_ranks(dist, elapsed, ok, dev)
 
-    enc_b, dec_b = alg_bytes(k, m, P)
-    value = aggregate_value(world, S, args.steps, k, m, P, elapsed)
+    enc_b, dec_b = alg_bytes(k, m, P, sys_)
+    value = aggregate_value(world, S, args.steps, k, m, P, elapsed, sys_)
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     enc_gbs = S * enc_b / (enc_ms * 1e-3) / 1e9
@@ -184,16 +200,25 @@ def main():
 
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    if headline and os.path.exists(pmc):
         try:
             with open(pmc) as f:
                 traffic = json.load(f).get("encode_bytes_per_launch")
         except Exception:
             traffic = None
 
+    K = 1
+    while K < k:
+        K *= 2
+    name = (f"RS-FNT{'-sys' if sys_ else ''} k={k} n={plan.n} "
+            f"pkt={pkt_bytes // 1024}KiB")
+    metric = ("device-resident encode+decode GB/s per GPU, RS-FNT k=16 n=64 "
+              "pkt=64KiB" if headline else
+              f"device-resident encode+decode GB/s per GPU, {name}")
+    enc_kernel = (f"encode_fnt_kernel<{K},*>" if not sys_ and K <= 64
+                  else "matrix_kernel<*>")
     out = {
-        "metric": "device-resident encode+decode GB/s per GPU, RS-FNT k=16 "
-                  "n=64 pkt=64KiB",
+        "metric": metric,
         "value": value,
         "unit": "GB/s",
         "n_gpus": world,
@@ -206,9 +231,9 @@ def main():
         "dtype": "u16",
         "data": "synthetic",
         "config": {
-            "workload": "RS-FNT k=16 n=64 pkt=64KiB encode+decode, "
-                        f"batch={S} stripes per GPU",
-            "k": k, "m": m, "n": plan.n, "pkt_bytes": PKT_BYTES,
+            "workload": f"{name} encode+decode, batch={S} stripes per GPU",
+            "k": k, "m": m, "n": plan.n, "pkt_bytes": pkt_bytes,
+            "systematic": sys_,
             "stripes_per_gpu": S,
             "decode": "per-stripe random n-k erasures, contexts built "
                       "on-GPU inside the timed step",
@@ -224,7 +249,7 @@ def main():
         "oor_max_per_bucket": oor_max,
         "roofline": {
             "bound": "hbm",
-            "kernel": "encode_fnt_kernel<16,*>",
+            "kernel": enc_kernel,
             "achieved": enc_gbs,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -236,7 +261,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        out["cpu_baseline"] = cpu_baseline(k, m, P, threads, args.cpu_stripes)
+        out["cpu_baseline"] = cpu_baseline(k, m, P, threads, args.cpu_stripes,
+                                           sys_)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -600,9 +600,15 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
 // src/fec_base.h:1361-1404, precomputed per tile).
 // One 64-lane workgroup per stripe; k <= 64.
 // ---------------------------------------------------------------------------
+// canonical a * b mod 65537 for a, b in [0, 65536]: with 2^16 = -1 and
+// 2^32 = 1, p = p0 + p1 2^16 + p2 2^32 reduces to p0 - p1 + p2
 __device__ __forceinline__ uint32_t mulm(uint32_t a, uint32_t b)
 {
-    return static_cast<uint32_t>((static_cast<uint64_t>(a) * b) % 65537u);
+    const uint64_t p = static_cast<uint64_t>(a) * b;
+    const int32_t v = static_cast<int32_t>(p & 0xffffu) -
+                      static_cast<int32_t>((p >> 16) & 0xffffu) +
+                      static_cast<int32_t>(p >> 32);  // [-65535, 65536]
+    return static_cast<uint32_t>(v < 0 ? v + 65537 : v);
 }
 __device__ __forceinline__ uint32_t addm(uint32_t a, uint32_t b)
 {
@@ -613,6 +619,16 @@ __device__ __forceinline__ uint32_t subm(uint32_t a, uint32_t b)
 {
     return a >= b ? a - b : a + 65537u - b;
 }
+__device__ __forceinline__ uint32_t powm(uint32_t b, uint32_t e)
+{
+    uint32_t r = 1;
+    for (; e; e >>= 1) {
+        if (e & 1)
+            r = mulm(r, b);
+        b = mulm(b, b);
+    }
+    return r;
+}
 
 __global__ __launch_bounds__(64) void decode_ctx_kernel(
     int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
@@ -622,6 +638,7 @@ __global__ __launch_bounds__(64) void decode_ctx_kernel(
     __shared__ uint32_t xs[64];
     __shared__ uint32_t A[65];
     __shared__ uint32_t Mt[64 * 64];
+    __shared__ uint32_t Qt[64 * 64];  // Q_i coefficients (systematic mode)
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
     int32_t* mat = ctx + s * ctx_stride;
@@ -636,7 +653,7 @@ __global__ __launch_bounds__(64) void decode_ctx_kernel(
         route[t * kRouteStride] = 0;
     if (tid < k) {
         const uint32_t id = ids[static_cast<long long>(s) * k + tid];
-        xs[tid] = powmod_c(r, id);
+        xs[tid] = powm(r, id);
         cids[tid] = static_cast<int32_t>(id);
     }
     __syncthreads();
@@ -659,37 +676,43 @@ __global__ __launch_bounds__(64) void decode_ctx_kernel(
             }
         }
     }
-    if (tid == 0) {
-        A[0] = 1;
-        for (int i = 0; i < k; i++) {
-            const uint32_t neg = subm(0, xs[i]);
-            A[i + 1] = A[i];
-            for (int d = i; d > 0; d--)
-                A[d] = addm(A[d - 1], mulm(A[d], neg));
-            A[0] = mulm(A[0], neg);
-        }
+    // A(x) = prod_i (x - x_i), lane d holding coefficient d (A is monic:
+    // A[k] = 1 is set explicitly, so k = 64 needs no 65th lane)
+    uint32_t a = tid == 0 ? 1u : 0u;
+    for (int i = 0; i < k; i++) {
+        uint32_t prev = __shfl_up(a, 1);
+        if (tid == 0)
+            prev = 0;
+        a = subm(prev, mulm(xs[i], a));
     }
+    A[tid] = a;
+    if (tid == 0)
+        A[k] = 1;
     __syncthreads();
     if (tid < k) {
+        // 1 / A'(x_i) = 1 / prod_{j != i} (x_i - x_j)
         const uint32_t xi = xs[tid];
-        uint32_t q[64];
-        q[k - 1] = A[k];
-        for (int j = k - 1; j >= 1; j--)
-            q[j - 1] = addm(A[j], mulm(xi, q[j]));
         uint32_t den = 1;
         for (int j = 0; j < k; j++)
             if (j != tid)
                 den = mulm(den, subm(xi, xs[j]));
-        const uint32_t inv = powmod_c(den, 65535u);
-        if (mode == 0) {
-            for (int t = 0; t < k; t++)
-                Mt[t * k + tid] = mulm(q[t], inv);
-        } else {
+        const uint32_t inv = powm(den, 65535u);
+        // Q_i = A / (x - x_i) by synthetic division from the top
+        uint32_t q = 1;  // A[k]
+        uint32_t* dst = mode == 0 ? Mt : Qt;
+        const uint32_t sc = mode == 0 ? inv : 1u;
+        dst[(k - 1) * k + tid] = sc;
+        for (int j = k - 1; j >= 1; j--) {
+            q = addm(A[j], mulm(xi, q));
+            dst[(j - 1) * k + tid] = mulm(q, sc);
+        }
+        if (mode != 0) {
+            // M[t][i] = Q_i(r^t) / A'(x_i)
             uint32_t e = 1;
             for (int t = 0; t < k; t++) {
                 uint32_t acc = 0;
                 for (int j = k - 1; j >= 0; j--)
-                    acc = addm(mulm(acc, e), q[j]);
+                    acc = addm(mulm(acc, e), Qt[j * k + tid]);
                 Mt[t * k + tid] = mulm(acc, inv);
                 e = mulm(e, r);
             }
