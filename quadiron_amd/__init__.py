@@ -17,7 +17,10 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libquadiron_amd.so")
+# QI_LIB_PATH: load another build of the same library (A/B timing of kernel
+# variants built by tools/ab_build.sh); the default is the in-tree product
+LIB_PATH = os.environ.get("QI_LIB_PATH") or os.path.join(HERE,
+                                                         "libquadiron_amd.so")
 
 _lib = None
 

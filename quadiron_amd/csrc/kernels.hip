@@ -75,8 +75,17 @@ struct Region {
     }
 };
 
+// Cache policy of the streamed rows (buffer-op aux bits): 2 = nt.  Measured
+// with tools/membw2.hip on the kernels' own shapes: nt stores +6 % on the
+// encode shape (16 rows in, 64 out); nt loads + stores +26 % on the decode
+// shape (16 of 64 rows in, 16 out); nt loads slow the encode shape down.
+#ifndef QI_AUX_NT
+#define QI_AUX_NT 2
+#endif
+constexpr int kAuxNT = QI_AUX_NT;
+
 // NDW (1 or 2) dwords per lane of the row at byte offset `row`
-template <int NDW, bool BUF>
+template <int NDW, bool BUF, int AUX = 0>
 __device__ __forceinline__ void ld_dw(const Region<BUF>& g, uint32_t row,
                                       uint32_t voff, uint32_t (&w)[NDW])
 {
@@ -84,13 +93,13 @@ __device__ __forceinline__ void ld_dw(const Region<BUF>& g, uint32_t row,
     if constexpr (NDW == 1) {
         if constexpr (BUF)
             w[0] = __builtin_amdgcn_raw_buffer_load_b32(
-                g.r, static_cast<int>(voff), static_cast<int>(row), 0);
+                g.r, static_cast<int>(voff), static_cast<int>(row), AUX);
         else
             w[0] = *reinterpret_cast<const uint32_t*>(g.p + row + voff);
     } else {
         if constexpr (BUF) {
             const auto v = __builtin_amdgcn_raw_buffer_load_b64(
-                g.r, static_cast<int>(voff), static_cast<int>(row), 0);
+                g.r, static_cast<int>(voff), static_cast<int>(row), AUX);
             w[0] = v[0];
             w[1] = v[1];
         } else {
@@ -101,7 +110,7 @@ __device__ __forceinline__ void ld_dw(const Region<BUF>& g, uint32_t row,
     }
 }
 
-template <int NDW, bool BUF>
+template <int NDW, bool BUF, int AUX = 0>
 __device__ __forceinline__ void st_dw(const Region<BUF>& g, uint32_t row,
                                       uint32_t voff, const uint32_t (&w)[NDW])
 {
@@ -109,7 +118,7 @@ __device__ __forceinline__ void st_dw(const Region<BUF>& g, uint32_t row,
     if constexpr (NDW == 1) {
         if constexpr (BUF)
             __builtin_amdgcn_raw_buffer_store_b32(w[0], g.r, static_cast<int>(voff),
-                                                  static_cast<int>(row), 0);
+                                                  static_cast<int>(row), AUX);
         else
             *reinterpret_cast<uint32_t*>(g.p + row + voff) = w[0];
     } else {
@@ -119,7 +128,7 @@ __device__ __forceinline__ void st_dw(const Region<BUF>& g, uint32_t row,
             v[0] = w[0];
             v[1] = w[1];
             __builtin_amdgcn_raw_buffer_store_b64(v, g.r, static_cast<int>(voff),
-                                                  static_cast<int>(row), 0);
+                                                  static_cast<int>(row), AUX);
         } else {
             *reinterpret_cast<uint2*>(g.p + row + voff) = make_uint2(w[0], w[1]);
         }
@@ -129,13 +138,13 @@ __device__ __forceinline__ void st_dw(const Region<BUF>& g, uint32_t row,
 // COLS adjacent u16 columns of the row at byte offset `row` (wave-uniform).
 // FULL: COLS/2 dwords per lane (COLS 2 or 4); otherwise one u16 per column
 // and columns past `avail` are 0.
-template <int COLS, bool FULL, bool BUF>
+template <int COLS, bool FULL, bool BUF, int AUX = 0>
 __device__ __forceinline__ void ld(const Region<BUF>& g, uint32_t row,
                                    uint32_t voff, long long avail, int32_t* v)
 {
     if constexpr (FULL && COLS % 2 == 0) {
         uint32_t w[COLS / 2];
-        ld_dw<COLS / 2, BUF>(g, row, voff, w);
+        ld_dw<COLS / 2, BUF, AUX>(g, row, voff, w);
 #pragma unroll
         for (int d = 0; d < COLS / 2; d++) {
             v[2 * d] = w[d] & 0xffff;
@@ -148,7 +157,7 @@ __device__ __forceinline__ void ld(const Region<BUF>& g, uint32_t row,
                 if constexpr (BUF)
                     v[c] = __builtin_amdgcn_raw_buffer_load_b16(
                         g.r, static_cast<int>(voff + 2 * c),
-                        static_cast<int>(row), 0);
+                        static_cast<int>(row), AUX);
                 else
                     v[c] = *reinterpret_cast<const uint16_t*>(g.p + row + voff +
                                                               2 * c);
@@ -159,7 +168,7 @@ __device__ __forceinline__ void ld(const Region<BUF>& g, uint32_t row,
     }
 }
 
-template <int COLS, bool FULL, bool BUF>
+template <int COLS, bool FULL, bool BUF, int AUX = 0>
 __device__ __forceinline__ void st(const Region<BUF>& g, uint32_t row,
                                    uint32_t voff, long long avail,
                                    const uint32_t* v)
@@ -169,7 +178,7 @@ __device__ __forceinline__ void st(const Region<BUF>& g, uint32_t row,
 #pragma unroll
         for (int d = 0; d < COLS / 2; d++)
             w[d] = pack_lo(v[2 * d], v[2 * d + 1]);
-        st_dw<COLS / 2, BUF>(g, row, voff, w);
+        st_dw<COLS / 2, BUF, AUX>(g, row, voff, w);
     } else {
 #pragma unroll
         for (int c = 0; c < COLS; c++) {
@@ -177,7 +186,7 @@ __device__ __forceinline__ void st(const Region<BUF>& g, uint32_t row,
                 if constexpr (BUF)
                     __builtin_amdgcn_raw_buffer_store_b16(
                         static_cast<uint16_t>(v[c]), g.r,
-                        static_cast<int>(voff + 2 * c), static_cast<int>(row), 0);
+                        static_cast<int>(voff + 2 * c), static_cast<int>(row), AUX);
                 else
                     *reinterpret_cast<uint16_t*>(g.p + row + voff + 2 * c) =
                         static_cast<uint16_t>(v[c]);
@@ -258,7 +267,7 @@ __device__ __forceinline__ void encode_body(
                 bad |= o[c];
             }
             if (row < n_out)
-                st<COLS, FULL, BUF>(go, static_cast<uint32_t>(row) * ors, voff,
+                st<COLS, FULL, BUF, kAuxNT>(go, static_cast<uint32_t>(row) * ors, voff,
                                     avail, o);
         }
         if (__builtin_expect((bad >> 16) != 0, 0)) {
@@ -279,7 +288,7 @@ __device__ __forceinline__ void encode_body(
                         mark |= 1ull << (u * COLS + c);
                 }
                 if (any && row < n_out)
-                    st<COLS, FULL, BUF>(go, static_cast<uint32_t>(row) * ors,
+                    st<COLS, FULL, BUF, kAuxNT>(go, static_cast<uint32_t>(row) * ors,
                                         voff, avail, o);
             }
             if (oor.counts) {
@@ -370,8 +379,8 @@ __device__ __forceinline__ void matrix_load(const int (&idv)[2 * KP],
         }
         if constexpr (FULL && COLS % 2 == 0) {
             uint32_t w0[COLS / 2], w1[COLS / 2];
-            ld_dw<COLS / 2, BUF>(g[0], off[0], voff, w0);
-            ld_dw<COLS / 2, BUF>(g[1], off[1], voff, w1);
+            ld_dw<COLS / 2, BUF, kAuxNT>(g[0], off[0], voff, w0);
+            ld_dw<COLS / 2, BUF, kAuxNT>(g[1], off[1], voff, w1);
 #pragma unroll
             for (int d = 0; d < COLS / 2; d++) {
                 xp[2 * d][j] = static_cast<int32_t>(
@@ -381,8 +390,8 @@ __device__ __forceinline__ void matrix_load(const int (&idv)[2 * KP],
             }
         } else {
             int32_t vv[2][COLS];
-            ld<COLS, FULL, BUF>(g[0], off[0], voff, avail, vv[0]);
-            ld<COLS, FULL, BUF>(g[1], off[1], voff, avail, vv[1]);
+            ld<COLS, FULL, BUF, kAuxNT>(g[0], off[0], voff, avail, vv[0]);
+            ld<COLS, FULL, BUF, kAuxNT>(g[1], off[1], voff, avail, vv[1]);
 #pragma unroll
             for (int c = 0; c < COLS; c++)
                 xp[c][j] = static_cast<int32_t>(
@@ -470,7 +479,7 @@ __device__ __forceinline__ void matrix_compute(
                 o[c] = fix16(y[c]);
             }
         }
-        st<COLS, FULL, BUF>(go, static_cast<uint32_t>(t) * ors, voff, avail, o);
+        st<COLS, FULL, BUF, kAuxNT>(go, static_cast<uint32_t>(t) * ors, voff, avail, o);
     }
 }
 

@@ -69,6 +69,34 @@ __global__ __launch_bounds__(256) void dec_shape(const uint16_t* in, uint16_t* o
     }
 }
 
+// pure streaming write / read of the coded-row footprint, 4 B per lane
+template <int AUX>
+__global__ __launch_bounds__(256) void wr_only(uint16_t* out, int tiles)
+{
+    const int b = blockIdx.x;
+    const int s = b / tiles, tile = b % tiles;
+    const uint32_t voff = (tile * 256 + threadIdx.x) * 4;
+    auto ro = rsrc(out + (long)s * 64 * P, 64 * P * 2);
+#pragma unroll
+    for (int u = 0; u < 64; u++)
+        __builtin_amdgcn_raw_buffer_store_b32(voff ^ u, ro, voff, u * P * 2, AUX);
+}
+
+__global__ __launch_bounds__(256) void rd_only(const uint16_t* in, uint32_t* sink,
+                                               int tiles)
+{
+    const int b = blockIdx.x;
+    const int s = b / tiles, tile = b % tiles;
+    const uint32_t voff = (tile * 256 + threadIdx.x) * 4;
+    auto ri = rsrc(in + (long)s * 64 * P, 64 * P * 2);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < 64; u++)
+        acc ^= __builtin_amdgcn_raw_buffer_load_b32(ri, voff, u * P * 2, 0);
+    if (acc == 0x12345678u)
+        sink[0] = acc;
+}
+
 template <typename F>
 float timeit(F f, int reps)
 {
@@ -107,6 +135,14 @@ int main(int argc, char** argv)
     {                                                                           \
         float ms = timeit([&] { dec_shape<L, S_><<<dt * S, 256>>>(b, a, dt); }, reps); \
         printf("dec shape aux L%d S%d  %7.3f ms %7.1f GB/s\n", L, S_, ms, db / ms / 1e6); \
+    }
+    {
+        float ms = timeit([&] { wr_only<0><<<et * S, 256>>>(b, et); }, reps);
+        printf("write-only 4B        %7.3f ms %7.1f GB/s\n", ms, bb / ms / 1e6);
+        ms = timeit([&] { wr_only<2><<<et * S, 256>>>(b, et); }, reps);
+        printf("write-only 4B nt     %7.3f ms %7.1f GB/s\n", ms, bb / ms / 1e6);
+        ms = timeit([&] { rd_only<<<et * S, 256>>>(b, reinterpret_cast<uint32_t*>(a), et); }, reps);
+        printf("read-only 4B         %7.3f ms %7.1f GB/s\n", ms, bb / ms / 1e6);
     }
     ENC(0, 0) ENC(0, 1) ENC(0, 2) ENC(0, 3) ENC(2, 0) ENC(2, 2)
     DEC(0, 0) DEC(0, 1) DEC(0, 2) DEC(0, 3) DEC(2, 0) DEC(2, 2)
