@@ -83,6 +83,12 @@ struct Region {
 #define QI_AUX_NT 2
 #endif
 constexpr int kAuxNT = QI_AUX_NT;
+// K values (bit log2 K) whose encode body re-reads its inputs every pass:
+// K = 32 (141 -> 105 VGPRs, 3 -> 4 waves/SIMD).  K = 64 stays resident (the
+// DFT64 codelet alone needs ~180 VGPRs, so reloading gains no occupancy).
+#ifndef QI_ENC_RELOAD_MASK
+#define QI_ENC_RELOAD_MASK (1 << 5)
+#endif
 
 // NDW (1 or 2) dwords per lane of the row at byte offset `row`
 template <int NDW, bool BUF, int AUX = 0>
@@ -215,19 +221,33 @@ __device__ __forceinline__ void encode_body(
     const Region<BUF>& gi, uint32_t irs, const Region<BUF>& go, uint32_t ors,
     uint32_t voff, long long col, long long avail, int s, const Oor& oor)
 {
+    // RELOAD (large K): re-read the K input rows every pass (L2 hits after
+    // the first) instead of keeping them live next to the pass's outputs --
+    // halves the VGPRs of the K = 32/64 bodies
+    constexpr bool RELOAD = ((QI_ENC_RELOAD_MASK) >> ilog2c(K)) & 1;
     int32_t x[COLS][K];
+    auto load_x = [&](uint32_t vo) {
 #pragma unroll
-    for (int t = 0; t < K; t++) {
-        const int row = KEQ ? t : (t < k ? t : k - 1);  // clamp, then mask
-        int32_t v[COLS];
-        ld<COLS, FULL, BUF>(gi, static_cast<uint32_t>(row) * irs, voff, avail, v);
+        for (int t = 0; t < K; t++) {
+            const int row = KEQ ? t : (t < k ? t : k - 1);  // clamp, then mask
+            int32_t v[COLS];
+            ld<COLS, FULL, BUF>(gi, static_cast<uint32_t>(row) * irs, vo, avail,
+                                v);
 #pragma unroll
-        for (int c = 0; c < COLS; c++)
-            x[c][t] = (KEQ || t < k) ? v[c] : 0;
-    }
+            for (int c = 0; c < COLS; c++)
+                x[c][t] = (KEQ || t < k) ? v[c] : 0;
+        }
+    };
+    if constexpr (!RELOAD)
+        load_x(voff);
 
     const int passes = n / K;
     for (int v = 0; v < passes; v++) {
+        if constexpr (RELOAD) {
+            uint32_t vo = voff;
+            asm volatile("" : "+v"(vo));  // keep the loads inside the loop
+            load_x(vo);
+        }
         int32_t y[COLS][K];
         if (v == 0) {
 #pragma unroll
@@ -307,7 +327,7 @@ __device__ __forceinline__ void encode_body(
 template <int K, int COLS, bool KEQ, bool BUF>
 // 4 waves per SIMD: the K=16, COLS=2 body fits 128 VGPRs without spills or
 // extra instructions (3 waves at the compiler's default 130)
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 64 ? 2 : 4))) void
 encode_fnt_kernel(
     int k, int n, int n_out, const int32_t* __restrict__ twist,
     const uint16_t* __restrict__ data, long long dss, uint32_t irs,
