@@ -97,6 +97,37 @@ __global__ __launch_bounds__(256) void rd_only(const uint16_t* in, uint32_t* sin
         sink[0] = acc;
 }
 
+
+// streaming write with W-byte stores per lane (W = 4, 8, 16)
+template <int W, int AUX>
+__global__ __launch_bounds__(256) void wr_wide(uint16_t* out, int tiles)
+{
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    const int b = blockIdx.x;
+    const int s = b / tiles, tile = b % tiles;
+    const uint32_t voff = (tile * 256 + threadIdx.x) * W;
+    auto ro = rsrc(out + (long)s * 64 * P, 64 * P * 2);
+#pragma unroll
+    for (int u = 0; u < 64; u++) {
+        if constexpr (W == 16)
+            __builtin_amdgcn_raw_buffer_store_b128(u4{voff ^ u, voff, (unsigned)u, 1u}, ro, voff, u * P * 2, AUX);
+        else if constexpr (W == 8)
+            __builtin_amdgcn_raw_buffer_store_b64(u2{voff ^ u, voff}, ro, voff, u * P * 2, AUX);
+        else
+            __builtin_amdgcn_raw_buffer_store_b32(voff ^ u, ro, voff, u * P * 2, AUX);
+    }
+}
+
+// plain contiguous copy, 16 B per lane (the guide's copy-kernel ceiling)
+__global__ __launch_bounds__(256) void copy16(const uint4* in, uint4* out, long n)
+{
+    long i = (long)blockIdx.x * 256 + threadIdx.x;
+    const long stride = (long)gridDim.x * 256;
+    for (; i < n; i += stride)
+        out[i] = in[i];
+}
+
 template <typename F>
 float timeit(F f, int reps)
 {
@@ -143,6 +174,18 @@ int main(int argc, char** argv)
         printf("write-only 4B nt     %7.3f ms %7.1f GB/s\n", ms, bb / ms / 1e6);
         ms = timeit([&] { rd_only<<<et * S, 256>>>(b, reinterpret_cast<uint32_t*>(a), et); }, reps);
         printf("read-only 4B         %7.3f ms %7.1f GB/s\n", ms, bb / ms / 1e6);
+    }
+
+    {
+        float ms = timeit([&] { wr_wide<8, 0><<<(P / 1024) * S, 256>>>(b, P / 1024); }, reps);
+        printf("write-only 8B        %7.3f ms %7.1f GB/s\n", ms, bb / ms / 1e6);
+        ms = timeit([&] { wr_wide<16, 0><<<(P / 2048) * S, 256>>>(b, P / 2048); }, reps);
+        printf("write-only 16B       %7.3f ms %7.1f GB/s\n", ms, bb / ms / 1e6);
+        ms = timeit([&] { wr_wide<16, 2><<<(P / 2048) * S, 256>>>(b, P / 2048); }, reps);
+        printf("write-only 16B nt    %7.3f ms %7.1f GB/s\n", ms, bb / ms / 1e6);
+        const long n16 = (long)ab / 16;
+        ms = timeit([&] { copy16<<<256 * 8 * 4, 256>>>((const uint4*)a, (uint4*)b, n16); }, reps);
+        printf("copy 16B (r+w)       %7.3f ms %7.1f GB/s\n", ms, 2.0 * ab / ms / 1e6);
     }
     ENC(0, 0) ENC(0, 1) ENC(0, 2) ENC(0, 3) ENC(2, 0) ENC(2, 2)
     DEC(0, 0) DEC(0, 1) DEC(0, 2) DEC(0, 3) DEC(2, 0) DEC(2, 2)
