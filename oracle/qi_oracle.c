@@ -441,6 +441,144 @@ int qo_decode_blocks(const qo_codec* c, uint8_t* const* data,
 }
 
 /* ------------------------------------------------------------------ */
+/* RS-NF4: src/fec_rs_nf4.h.  NF4<T> (src/gf_nf4.h:116-132) is the ring of
+ * gf_n = word_size/2 tuples over GF(65537) with componentwise arithmetic
+ * (:214-316); the code uses the prime field's n-th root replicated in every
+ * component (get_nth_root :450-455) and the same Radix2 transforms as RsFnt
+ * (src/fec_rs_nf4.h:78-96).  So component c of word j -- the 16-bit lane
+ * j*g + c of the byte stream (vec::pack word_size bytes per word, then
+ * NF4::pack :355-365) -- is one RS-FNT column.  encode_post_process
+ * (src/fec_rs_nf4.h:271-289, NF4::unpack :391-446) records, per output and
+ * word, the bitmask of components equal to 65536 (stored as 0);
+ * decode_prepare (:291-317, NF4::pack(a, flag) :372-383) restores them. */
+
+void qo_nf4_encode_blocks(const qo_codec* c, int word_size,
+                          uint8_t* const* data, uint8_t* const* outputs,
+                          size_t block_bytes, uint32_t* oor, uint32_t* flags,
+                          uint32_t* oor_count, uint32_t oor_cap)
+{
+    const int g = word_size / 2, k = c->k, no = c->n_outputs;
+    const size_t words = block_bytes / (size_t)word_size; /* fec_base.h:1083 */
+    uint32_t in[1024];
+    uint32_t* cw = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)c->n);
+    uint32_t* mask = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)no);
+    size_t j;
+    int comp, i;
+
+    for (i = 0; i < no; i++)
+        oor_count[i] = 0;
+    for (j = 0; j < words; j++) {
+        for (i = 0; i < no; i++)
+            mask[i] = 0;
+        for (comp = 0; comp < g; comp++) {
+            const size_t lane = j * (size_t)g + (size_t)comp;
+            for (i = 0; i < k; i++)
+                in[i] = (uint32_t)data[i][2 * lane] |
+                        ((uint32_t)data[i][2 * lane + 1] << 8);
+            qo_encode_column(c, NULL, in, cw);
+            for (i = 0; i < no; i++) {
+                const uint32_t v = cw[i];
+                if (v & 65536u)
+                    mask[i] |= 1u << comp;
+                if (outputs[i]) {
+                    outputs[i][2 * lane] = (uint8_t)v;
+                    outputs[i][2 * lane + 1] = (uint8_t)(v >> 8);
+                }
+            }
+        }
+        for (i = 0; i < no; i++) {
+            if (!mask[i])
+                continue;
+            if (oor_count[i] < oor_cap) {
+                oor[(size_t)i * oor_cap + oor_count[i]] = (uint32_t)j;
+                flags[(size_t)i * oor_cap + oor_count[i]] = mask[i];
+            }
+            oor_count[i]++;
+        }
+    }
+    free(mask);
+    free(cw);
+}
+
+static int cmp_u64(const void* a, const void* b)
+{
+    uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+int qo_nf4_decode_blocks(const qo_codec* c, int word_size,
+                         uint8_t* const* data, uint8_t* const* parities,
+                         const uint32_t* oor, const uint32_t* flags,
+                         const uint32_t* oor_count, uint32_t oor_cap,
+                         const int* missing, const int* wanted,
+                         size_t block_bytes)
+{
+    const int g = word_size / 2, k = c->k;
+    const size_t words = block_bytes / (size_t)word_size;
+    uint32_t ids[1024] = {0};
+    const uint8_t* src[1024];
+    uint64_t* marks[1024]; /* word << 8 | component mask, sorted */
+    uint32_t nmarks[1024], pos[1024], cur[1024];
+    uint32_t in[1024], out[1024];
+    int i, fi = 0, comp;
+    size_t j, e;
+    qo_ctx* ctx;
+
+    /* first k present fragments (src/fec_base.h:1217-1236, non-systematic) */
+    for (i = 0; i < c->n_outputs && fi < k; i++) {
+        if (!missing[i]) {
+            const uint32_t n = oor_count[i] < oor_cap ? oor_count[i] : oor_cap;
+            ids[fi] = (uint32_t)i;
+            src[fi] = parities[i];
+            marks[fi] = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+            for (e = 0; e < n; e++)
+                marks[fi][e] = ((uint64_t)oor[(size_t)i * oor_cap + e] << 8) |
+                               flags[(size_t)i * oor_cap + e];
+            qsort(marks[fi], n, sizeof(uint64_t), cmp_u64); /* fec_context.h:93-97 */
+            nmarks[fi] = n;
+            pos[fi] = 0;
+            fi++;
+        }
+    }
+    if (fi < k) {
+        for (i = 0; i < fi; i++)
+            free(marks[i]);
+        return 0;
+    }
+    ctx = (qo_ctx*)malloc(sizeof(qo_ctx));
+    qo_ctx_init(c, ctx, ids);
+    for (j = 0; j < words; j++) {
+        for (i = 0; i < k; i++) {
+            cur[i] = 0;
+            while (pos[i] < nmarks[i] && (marks[i][pos[i]] >> 8) < j)
+                pos[i]++;
+            while (pos[i] < nmarks[i] && (marks[i][pos[i]] >> 8) == j)
+                cur[i] |= (uint32_t)(marks[i][pos[i]++] & 0xffu);
+        }
+        for (comp = 0; comp < g; comp++) {
+            const size_t lane = j * (size_t)g + (size_t)comp;
+            for (i = 0; i < k; i++) {
+                in[i] = (uint32_t)src[i][2 * lane] |
+                        ((uint32_t)src[i][2 * lane + 1] << 8);
+                if ((cur[i] >> comp) & 1u)
+                    in[i] = 65536u; /* NF4::pack(a, flag) */
+            }
+            qo_decode_column(c, ctx, in, out);
+            for (i = 0; i < k; i++) {
+                if (wanted[i]) {
+                    data[i][2 * lane] = (uint8_t)out[i];
+                    data[i][2 * lane + 1] = (uint8_t)(out[i] >> 8);
+                }
+            }
+        }
+    }
+    for (i = 0; i < k; i++)
+        free(marks[i]);
+    free(ctx);
+    return 1;
+}
+
+/* ------------------------------------------------------------------ */
 /* C-ABI semantics: src/quadiron_c.cpp */
 
 int qo_metadata_size(size_t block_size)

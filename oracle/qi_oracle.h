@@ -94,6 +94,25 @@ int qo_decode_blocks(const qo_codec* c, uint8_t* const* data,
                      const int* missing, const int* wanted,
                      size_t block_bytes);
 
+/* ---- RS-NF4 block API (src/fec_rs_nf4.h:46-334, src/gf_nf4.h) ----
+ * word_size in {2, 4, 8}: word j of a fragment packs word_size/2 GF(65537)
+ * components (the 16-bit lanes j*g .. j*g+g-1 of the byte stream), each
+ * coded like an RS-FNT column.  c: a NON-systematic codec (qo_codec_init
+ * with sys = 0).  OOR marks per output: ascending word offsets in `oor`,
+ * component bitmasks in `flags` (cap entries each, counts exact).  Only
+ * whole words (block_bytes / word_size) are processed. */
+void qo_nf4_encode_blocks(const qo_codec* c, int word_size,
+                          uint8_t* const* data, uint8_t* const* outputs,
+                          size_t block_bytes, uint32_t* oor, uint32_t* flags,
+                          uint32_t* oor_count, uint32_t oor_cap);
+/* missing: code_len flags (nonzero = missing).  1 decoded, 0 < k present. */
+int qo_nf4_decode_blocks(const qo_codec* c, int word_size,
+                         uint8_t* const* data, uint8_t* const* parities,
+                         const uint32_t* oor, const uint32_t* flags,
+                         const uint32_t* oor_count, uint32_t oor_cap,
+                         const int* missing, const int* wanted,
+                         size_t block_bytes);
+
 /* ---- C-ABI semantics (src/quadiron_c.cpp:37-406) ---- */
 int qo_metadata_size(size_t block_size);
 int qo_fnt32_encode(const qo_codec* c, uint8_t** data, uint8_t** parity,

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "fec_rs_fnt.h"
+#include "fec_rs_nf4.h"
 #include "property.h"
 
 using quadiron::Properties;
@@ -49,6 +50,67 @@ void props_out(const Properties& p, uint32_t* list, uint32_t* count,
 int md_size(size_t block_size)
 {
     return static_cast<int>(((block_size / 65536) + 16) * 4);
+}
+
+template <typename T>
+void nf4_encode(int ws, int k, int m, size_t pkt, uint8_t** data,
+                uint8_t** outputs, size_t block_bytes, uint32_t* oor,
+                uint32_t* flags, uint32_t* oor_count, uint32_t cap)
+{
+    quadiron::fec::RsNf4<T> f(ws, k, m, pkt);
+    unsigned no = f.n_outputs;
+    std::vector<uint8_t*> dv(data, data + k);
+    std::vector<uint8_t*> pv(no);
+    std::vector<Properties> props(no);
+    std::vector<bool> wanted(no);
+    std::vector<std::vector<uint8_t>> scratch(no);
+    for (unsigned i = 0; i < no; i++) {
+        wanted[i] = outputs[i] != nullptr;
+        if (!outputs[i]) {
+            scratch[i].resize(block_bytes + 16);
+            pv[i] = scratch[i].data();
+        } else {
+            pv[i] = outputs[i];
+        }
+    }
+    f.encode_blocks_vertical(dv, pv, props, wanted, block_bytes);
+    for (unsigned i = 0; i < no; i++) {
+        uint32_t c = 0;
+        for (auto const& it : props[i].get_map()) {
+            if (c < cap) {
+                oor[static_cast<size_t>(i) * cap + c] =
+                    static_cast<uint32_t>(it.first);
+                flags[static_cast<size_t>(i) * cap + c] = it.second;
+            }
+            c++;
+        }
+        oor_count[i] = c;
+    }
+}
+
+template <typename T>
+int nf4_decode(int ws, int k, int m, size_t pkt, uint8_t** data,
+               uint8_t** parities, const uint32_t* oor, const uint32_t* flags,
+               const uint32_t* oor_count, uint32_t cap, const int* missing,
+               const int* wanted, size_t block_bytes)
+{
+    quadiron::fec::RsNf4<T> f(ws, k, m, pkt);
+    unsigned no = f.n_outputs;
+    std::vector<uint8_t*> dv(data, data + k);
+    std::vector<uint8_t*> pv(parities, parities + no);
+    std::vector<Properties> props(no);
+    std::vector<int> miss(missing, missing + no);
+    std::vector<bool> want(k);
+    for (int i = 0; i < k; i++)
+        want[i] = wanted[i] != 0;
+    for (unsigned i = 0; i < no; i++) {
+        uint32_t c = oor_count[i] < cap ? oor_count[i] : cap;
+        for (uint32_t e = 0; e < c; e++)
+            props[i].add(oor[static_cast<size_t>(i) * cap + e],
+                         flags[static_cast<size_t>(i) * cap + e]);
+    }
+    return f.decode_blocks_vertical(dv, pv, props, miss, want, block_bytes) ? 1
+                                                                            : 0;
 }
 
 } // namespace
@@ -302,6 +364,53 @@ int ref_c_reconstruct(int sys, int k, int m, uint8_t** data, uint8_t** parity,
                                   md / 4) == -1
                ? -1
                : 0;
+}
+
+/*
+ * RS-NF4 (src/fec_rs_nf4.h): RsNf4<T>(word_size, k, m, pkt) with the word
+ * type the reference benchmark picks (benchmark/benchmark.cpp:283-306,
+ * 696-718: sizeof(T) >= 2 * word_size), through the same vertical block API.
+ * OOR marks are (word offset, component flag) pairs.
+ */
+int ref_nf4_n_outputs(int ws, int k, int m)
+{
+    if (ws == 2)
+        return quadiron::fec::RsNf4<uint32_t>(ws, k, m, 8).n_outputs;
+    if (ws == 4)
+        return quadiron::fec::RsNf4<uint64_t>(ws, k, m, 8).n_outputs;
+    return quadiron::fec::RsNf4<__uint128_t>(ws, k, m, 8).n_outputs;
+}
+
+void ref_nf4_encode_blocks(int ws, int k, int m, size_t pkt, uint8_t** data,
+                           uint8_t** outputs, size_t block_bytes, uint32_t* oor,
+                           uint32_t* flags, uint32_t* oor_count, uint32_t cap)
+{
+    if (ws == 2)
+        nf4_encode<uint32_t>(ws, k, m, pkt, data, outputs, block_bytes, oor,
+                             flags, oor_count, cap);
+    else if (ws == 4)
+        nf4_encode<uint64_t>(ws, k, m, pkt, data, outputs, block_bytes, oor,
+                             flags, oor_count, cap);
+    else
+        nf4_encode<__uint128_t>(ws, k, m, pkt, data, outputs, block_bytes, oor,
+                                flags, oor_count, cap);
+}
+
+/* `missing`: code_len (= n_outputs, non-systematic) flags, nonzero = missing */
+int ref_nf4_decode_blocks(int ws, int k, int m, size_t pkt, uint8_t** data,
+                          uint8_t** parities, const uint32_t* oor,
+                          const uint32_t* flags, const uint32_t* oor_count,
+                          uint32_t cap, const int* missing, const int* wanted,
+                          size_t block_bytes)
+{
+    if (ws == 2)
+        return nf4_decode<uint32_t>(ws, k, m, pkt, data, parities, oor, flags,
+                                    oor_count, cap, missing, wanted, block_bytes);
+    if (ws == 4)
+        return nf4_decode<uint64_t>(ws, k, m, pkt, data, parities, oor, flags,
+                                    oor_count, cap, missing, wanted, block_bytes);
+    return nf4_decode<__uint128_t>(ws, k, m, pkt, data, parities, oor, flags,
+                                   oor_count, cap, missing, wanted, block_bytes);
 }
 
 /*

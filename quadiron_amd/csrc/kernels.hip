@@ -75,17 +75,53 @@ struct Region {
     }
 };
 
-// Cache policy of the streamed rows (buffer-op aux bits): 2 = nt.  Measured
-// with tools/membw2.hip on the kernels' own shapes: nt stores +6 % on the
-// encode shape (16 rows in, 64 out); nt loads + stores +26 % on the decode
-// shape (16 of 64 rows in, 16 out); nt loads slow the encode shape down.
-#ifndef QI_AUX_NT
-#define QI_AUX_NT 2
+// Cache policy of the streamed rows (buffer-op aux bits on gfx950: 1 = sc0,
+// 2 = nt, 16 = sc1).  Measured with tools/membw2.hip / membw3.hip on the
+// kernels' own shapes (profiles/r1_membw.txt): nt|sc1 stores (device scope,
+// written through the XCD's L2) +5 % on both the encode shape (16 rows in,
+// 64 out) and the decode shape (16 of 64 rows in, 16 out); nt loads +5 % on
+// the decode shape, but slow the encode shape down (its inputs stay plain).
+#ifndef QI_AUX_LD
+#define QI_AUX_LD 2
 #endif
-constexpr int kAuxNT = QI_AUX_NT;
+#ifndef QI_AUX_ST
+#define QI_AUX_ST 18
+#endif
+constexpr int kAuxLd = QI_AUX_LD;
+constexpr int kAuxSt = QI_AUX_ST;
+
+// XCD-aware block -> (stripe, tile) map.  Workgroups are dispatched
+// round-robin over the 8 XCDs (block b runs on XCD b % 8), so with the plain
+// stripe-major order the 8 adjacent tiles of one stripe land on 8 different
+// XCDs.  Instead, each group of 8 consecutive stripes is split so that XCD x
+// walks all tiles of stripe 8g + x: +4-6 % HBM throughput on both kernel
+// shapes (membw3 "ord3").  A trailing partial group (S % 8 stripes) keeps
+// the stripe-major order.
+#ifndef QI_XCD_MAP
+#define QI_XCD_MAP 1
+#endif
+__device__ __forceinline__ void block_map(int b, int tiles, int& s, int& tile)
+{
+    if constexpr (QI_XCD_MAP) {
+        const int n_stripes = static_cast<int>(gridDim.x) / tiles;
+        const int grouped = (n_stripes & ~7) * tiles;  // blocks in full groups
+        if (b < grouped) {
+            const int j = b >> 3;
+            const int g = j / tiles;
+            s = g * 8 + (b & 7);
+            tile = j - g * tiles;
+            return;
+        }
+    }
+    s = b / tiles;
+    tile = b - s * tiles;
+}
 // K values (bit log2 K) whose encode body re-reads its inputs every pass:
 // K = 32 (141 -> 105 VGPRs, 3 -> 4 waves/SIMD).  K = 64 stays resident (the
 // DFT64 codelet alone needs ~180 VGPRs, so reloading gains no occupancy).
+#ifndef QI_ENC_PAIR
+#define QI_ENC_PAIR 0
+#endif
 #ifndef QI_ENC_RELOAD_MASK
 #define QI_ENC_RELOAD_MASK (1 << 5)
 #endif
@@ -225,36 +261,66 @@ __device__ __forceinline__ void encode_body(
     // the first) instead of keeping them live next to the pass's outputs --
     // halves the VGPRs of the K = 32/64 bodies
     constexpr bool RELOAD = ((QI_ENC_RELOAD_MASK) >> ilog2c(K)) & 1;
-    int32_t x[COLS][K];
+    // PAIRED (full tiles, 2 columns per lane): passes 2w and 2w+1 are stored
+    // together, row 4u+2w then 4u+2w+1, ...  Storing a pass alone writes 16
+    // rows that share the row-index bits below log2(passes) -- the 64 KiB
+    // address bit(s) -- and measures 7 % slower in HBM than storing rows with
+    // that bit alternating (membw3 "ro1" vs "ro2").  The inputs are then kept
+    // as the loaded u16 pairs (K dwords, unpacked at use) to pay for the K
+    // held dwords of the even pass.
+    constexpr bool PAIRED = QI_ENC_PAIR && FULL && COLS == 2 && !RELOAD;
+    const int passes = n / K;
+    const bool paired = PAIRED && (passes & 1) == 0;  // uniform
+
+    uint32_t xw[PAIRED ? K : 1];  // PAIRED: [col1 | col0] per input row
+    int32_t x[PAIRED ? 1 : COLS][K];
     auto load_x = [&](uint32_t vo) {
 #pragma unroll
         for (int t = 0; t < K; t++) {
             const int row = KEQ ? t : (t < k ? t : k - 1);  // clamp, then mask
-            int32_t v[COLS];
-            ld<COLS, FULL, BUF>(gi, static_cast<uint32_t>(row) * irs, vo, avail,
-                                v);
+            if constexpr (PAIRED) {
+                uint32_t w[1];
+                ld_dw<1, BUF>(gi, static_cast<uint32_t>(row) * irs, vo, w);
+                xw[t] = (KEQ || t < k) ? w[0] : 0u;
+            } else {
+                int32_t v[COLS];
+                ld<COLS, FULL, BUF>(gi, static_cast<uint32_t>(row) * irs, vo, avail,
+                                    v);
 #pragma unroll
-            for (int c = 0; c < COLS; c++)
-                x[c][t] = (KEQ || t < k) ? v[c] : 0;
+                for (int c = 0; c < COLS; c++)
+                    x[c][t] = (KEQ || t < k) ? v[c] : 0;
+            }
         }
+    };
+    auto xin = [&](int c, int t) -> int32_t {
+        if constexpr (PAIRED)
+            return static_cast<int32_t>(c == 0 ? xw[t] & 0xffffu : xw[t] >> 16);
+        else
+            return x[c][t];
     };
     if constexpr (!RELOAD)
         load_x(voff);
 
-    const int passes = n / K;
-    for (int v = 0; v < passes; v++) {
+    // pass v: y[c][u] = output row passes*u + v of column c, in V = [-2, 65537]
+    auto compute = [&](int v, int32_t (&y)[COLS][K]) {
         if constexpr (RELOAD) {
             uint32_t vo = voff;
             asm volatile("" : "+v"(vo));  // keep the loads inside the loop
             load_x(vo);
         }
-        int32_t y[COLS][K];
+        if constexpr (PAIRED) {
+            // opaque per pass: keeps the unpacking inside the pass (hoisted,
+            // the 2K unpacked inputs would stay live and spill)
+#pragma unroll
+            for (int t = 0; t < K; t++)
+                asm volatile("" : "+v"(xw[t]));
+        }
         if (v == 0) {
 #pragma unroll
             for (int c = 0; c < COLS; c++) {
 #pragma unroll
                 for (int t = 0; t < K; t++)
-                    y[c][t] = x[c][t];
+                    y[c][t] = xin(c, t);
                 dft<K, 0, 65535>(y[c]);
             }
         } else {
@@ -267,61 +333,108 @@ __device__ __forceinline__ void encode_body(
                 const int32_t cb = tw[t];
 #pragma unroll
                 for (int c = 0; c < COLS; c++)
-                    y[c][t] = t == 0 ? x[c][t] : fold(mul_i24_s(x[c][t], cb));
+                    y[c][t] = t == 0 ? xin(c, t) : fold(mul_i24_s(xin(c, t), cb));
             }
 #pragma unroll
             for (int c = 0; c < COLS; c++)
                 dft<K, kTwLo, kTwHi>(y[c]);
         }
-        // outputs are in V = [-2, 65537]: the fast path stores the low 16
-        // bits; any value outside [0, 65535] (the true OOR symbol 65536 or a
-        // non-canonical alias) sends the pass through the fix-up below
+    };
+    // the stored word is the low 16 bits; any output outside [0, 65535] (the
+    // true OOR symbol 65536 or a non-canonical alias) sends the pass through
+    // the rare fix-up: canonicalise in place, then record the OOR marks from
+    // a bitmask (keeps the atomics out of the unrolled code)
+    auto fixup = [&](int v, int32_t (&y)[COLS][K]) {
         uint32_t bad = 0;
 #pragma unroll
-        for (int u = 0; u < K; u++) {
-            const int row = passes * u + v;
-            uint32_t o[COLS];
+        for (int u = 0; u < K; u++)
 #pragma unroll
-            for (int c = 0; c < COLS; c++) {
-                o[c] = static_cast<uint32_t>(y[c][u]);
-                bad |= o[c];
-            }
-            if (row < n_out)
-                st<COLS, FULL, BUF, kAuxNT>(go, static_cast<uint32_t>(row) * ors, voff,
-                                    avail, o);
-        }
+            for (int c = 0; c < COLS; c++)
+                bad |= static_cast<uint32_t>(y[c][u]);
         if (__builtin_expect((bad >> 16) != 0, 0)) {
-            // fix the stored words of this pass, then record the OOR marks
-            // from a bitmask (keeps the atomics out of the unrolled code)
             uint64_t mark = 0;
 #pragma unroll
             for (int u = 0; u < K; u++) {
-                const int row = passes * u + v;
-                uint32_t any = 0;
-                uint32_t o[COLS];
 #pragma unroll
                 for (int c = 0; c < COLS; c++) {
                     const uint32_t cv = canon_v(y[c][u]);
-                    o[c] = cv & 0xffffu;
-                    any |= static_cast<uint32_t>(y[c][u]) >> 16;
+                    y[c][u] = static_cast<int32_t>(cv & 0xffffu);
                     if (cv == 65536u && (FULL || c < avail))
                         mark |= 1ull << (u * COLS + c);
                 }
-                if (any && row < n_out)
-                    st<COLS, FULL, BUF, kAuxNT>(go, static_cast<uint32_t>(row) * ors,
-                                        voff, avail, o);
             }
             if (oor.counts) {
                 while (mark) {
-                    const int b = __builtin_ctzll(mark);
+                    const int bit = __builtin_ctzll(mark);
                     mark &= mark - 1;
-                    const int row = passes * (b / COLS) + v;
+                    const int row = passes * (bit / COLS) + v;
                     if (row < n_out)
-                        record_oor(oor, s, row, col + (b % COLS));
+                        record_oor(oor, s, row, col + (bit % COLS));
                 }
             }
         }
+    };
+    // CHK: some rows >= n_out are not wanted (uniform per launch; the
+    // checks become a scalar branch around every store, so the common
+    // all-rows case gets its own branch-free copy)
+    auto store_row = [&](auto chk, int row, const int32_t (&y)[COLS][K], int u) {
+        uint32_t o[COLS];
+#pragma unroll
+        for (int c = 0; c < COLS; c++)
+            o[c] = static_cast<uint32_t>(y[c][u]);
+        if (!decltype(chk)::value || row < n_out)
+            st<COLS, FULL, BUF, kAuxSt>(go, static_cast<uint32_t>(row) * ors, voff,
+                                        avail, o);
+    };
+    auto run_paired = [&](auto chk) {
+        for (int v = 0; v < passes; v += 2) {
+            int32_t y[COLS][K];
+            compute(v, y);
+            fixup(v, y);
+            uint32_t held[K];
+#pragma unroll
+            for (int u = 0; u < K; u++)
+                held[u] = pack_lo(static_cast<uint32_t>(y[0][u]),
+                                  static_cast<uint32_t>(y[1][u]));
+            compute(v + 1, y);
+            fixup(v + 1, y);
+#pragma unroll
+            for (int u = 0; u < K; u++) {
+                const int row = passes * u + v;
+                if (!decltype(chk)::value || row < n_out) {
+                    const uint32_t w[1] = {held[u]};
+                    st_dw<1, BUF, kAuxSt>(go, static_cast<uint32_t>(row) * ors, voff,
+                                          w);
+                }
+                store_row(chk, row + 1, y, u);
+            }
+        }
+    };
+    auto run = [&](auto chk) {
+        for (int v = 0; v < passes; v++) {
+            int32_t y[COLS][K];
+            compute(v, y);
+            fixup(v, y);
+#pragma unroll
+            for (int u = 0; u < K; u++)
+                store_row(chk, passes * u + v, y, u);
+        }
+    };
+    using all_rows = std::integral_constant<bool, false>;
+    using some_rows = std::integral_constant<bool, true>;
+    if constexpr (PAIRED) {
+        if (paired) {
+            if (n_out >= n)
+                run_paired(all_rows{});
+            else
+                run_paired(some_rows{});
+            return;
+        }
     }
+    if (n_out >= n)
+        run(all_rows{});
+    else
+        run(some_rows{});
 }
 
 template <int K, int COLS, bool KEQ, bool BUF>
@@ -334,9 +447,8 @@ encode_fnt_kernel(
     uint32_t iext, uint16_t* __restrict__ out, long long oss, uint32_t ors,
     uint32_t oext, long long words, int tiles, Oor oor)
 {
-    const int b = blockIdx.x;
-    const int s = b / tiles;
-    const int tile = b - s * tiles;
+    int s, tile;
+    block_map(blockIdx.x, tiles, s, tile);
     const long long col0 = static_cast<long long>(tile) * kBlock * COLS;
     const long long col = col0 + static_cast<long long>(threadIdx.x) * COLS;
     const Region<BUF> gi(data + s * dss, iext);
@@ -399,8 +511,8 @@ __device__ __forceinline__ void matrix_load(const int (&idv)[2 * KP],
         }
         if constexpr (FULL && COLS % 2 == 0) {
             uint32_t w0[COLS / 2], w1[COLS / 2];
-            ld_dw<COLS / 2, BUF, kAuxNT>(g[0], off[0], voff, w0);
-            ld_dw<COLS / 2, BUF, kAuxNT>(g[1], off[1], voff, w1);
+            ld_dw<COLS / 2, BUF, kAuxLd>(g[0], off[0], voff, w0);
+            ld_dw<COLS / 2, BUF, kAuxLd>(g[1], off[1], voff, w1);
 #pragma unroll
             for (int d = 0; d < COLS / 2; d++) {
                 xp[2 * d][j] = static_cast<int32_t>(
@@ -410,8 +522,8 @@ __device__ __forceinline__ void matrix_load(const int (&idv)[2 * KP],
             }
         } else {
             int32_t vv[2][COLS];
-            ld<COLS, FULL, BUF, kAuxNT>(g[0], off[0], voff, avail, vv[0]);
-            ld<COLS, FULL, BUF, kAuxNT>(g[1], off[1], voff, avail, vv[1]);
+            ld<COLS, FULL, BUF, kAuxLd>(g[0], off[0], voff, avail, vv[0]);
+            ld<COLS, FULL, BUF, kAuxLd>(g[1], off[1], voff, avail, vv[1]);
 #pragma unroll
             for (int c = 0; c < COLS; c++)
                 xp[c][j] = static_cast<int32_t>(
@@ -499,7 +611,7 @@ __device__ __forceinline__ void matrix_compute(
                 o[c] = fix16(y[c]);
             }
         }
-        st<COLS, FULL, BUF, kAuxNT>(go, static_cast<uint32_t>(t) * ors, voff, avail, o);
+        st<COLS, FULL, BUF, kAuxSt>(go, static_cast<uint32_t>(t) * ors, voff, avail, o);
     }
 }
 
@@ -515,9 +627,8 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
     __shared__ int s_i[kMaxTileOor];
     __shared__ uint32_t s_col[kMaxTileOor];
 
-    const int b = blockIdx.x;
-    const int s = b / tiles;
-    const int tile = b - s * tiles;
+    int s, tile;
+    block_map(blockIdx.x, tiles, s, tile);
     const int kin = L.kin;
     const long long col0 = static_cast<long long>(tile) * kBlock * COLS;
     const long long col1 = col0 + kBlock * COLS;
