@@ -97,3 +97,33 @@ def oracle_decode_blocks(k, m, sys_, outputs, oor, cnt, missing, data=None):
                                    vp(cnt), C.c_uint32(oor.shape[1]),
                                    vp(missing), vp(wanted), C.c_size_t(B))
     return ok, np.stack(dec)
+
+
+def oracle_nf4_encode_blocks(ws, k, m, data, cap):
+    """RS-NF4 (oracle): data (k, B) uint8 -> outputs, oor words, flags, cnt."""
+    c = codec(k, m, 0)
+    B = data.shape[1]
+    outs = np.zeros((c.n_outputs, B), np.uint8)
+    oor = np.zeros((c.n_outputs, cap), np.uint32)
+    flags = np.zeros((c.n_outputs, cap), np.uint32)
+    cnt = np.zeros(c.n_outputs, np.uint32)
+    rows = [np.ascontiguousarray(data[i]) for i in range(k)]
+    oracle().qo_nf4_encode_blocks(C.byref(c), ws, ptrs(rows),
+                                  ptrs([outs[i] for i in range(c.n_outputs)]),
+                                  C.c_size_t(B), vp(oor), vp(flags), vp(cnt),
+                                  C.c_uint32(cap))
+    return outs, oor, flags, cnt
+
+
+def oracle_nf4_decode_blocks(ws, k, m, outputs, oor, flags, cnt, missing):
+    c = codec(k, m, 0)
+    B = outputs.shape[1]
+    dec = [np.zeros(B, np.uint8) for _ in range(k)]
+    par = [None if missing[i] else outputs[i].copy()
+           for i in range(c.n_outputs)]
+    missing = np.ascontiguousarray(missing, np.int32)
+    wanted = np.ones(k, np.int32)
+    ok = oracle().qo_nf4_decode_blocks(
+        C.byref(c), ws, ptrs(dec), ptrs(par), vp(oor), vp(flags), vp(cnt),
+        C.c_uint32(oor.shape[1]), vp(missing), vp(wanted), C.c_size_t(B))
+    return ok, np.stack(dec)

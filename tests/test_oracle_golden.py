@@ -8,7 +8,9 @@ import numpy as np
 import pytest
 
 from qi_testlib import (Q, codec, golden_names, load, oracle,
-                        oracle_decode_blocks, oracle_encode_blocks, ptrs, vp)
+                        oracle_decode_blocks, oracle_encode_blocks,
+                        oracle_nf4_decode_blocks, oracle_nf4_encode_blocks,
+                        ptrs, vp)
 
 
 def naive_dft(x, w):
@@ -114,6 +116,24 @@ def test_oracle_cabi_vs_reference(name):
         assert o.qo_fnt32_reconstruct(C.byref(c), ptrs(D), ptrs(P), vp(miss),
                                       C.c_uint(dest), C.c_size_t(B)) == 0
         assert ((D + P)[dest] == g["reconstructed"][t]).all()
+
+
+@pytest.mark.parametrize("name", golden_names("nf4_"))
+def test_oracle_nf4_vs_reference(name):
+    """RS-NF4 (src/fec_rs_nf4.h) restated as per-lane RS-FNT + (word,
+    component-mask) marks, against RsNf4<T> outputs."""
+    g = load(name)
+    ws, k, m, pkt, B, cap = (int(v) for v in g["params"])
+    outs, oor, flags, cnt = oracle_nf4_encode_blocks(ws, k, m, g["data"], cap)
+    assert (outs == g["outputs"]).all()
+    assert (cnt == g["oor_count"]).all()
+    assert (oor == g["oor"]).all() and (flags == g["flags"]).all()
+    for p in range(len(g["missing"])):
+        ok, dec = oracle_nf4_decode_blocks(ws, k, m, g["outputs"], g["oor"],
+                                           g["flags"], g["oor_count"],
+                                           g["missing"][p])
+        assert ok == 1
+        assert (dec == g["decoded"][p]).all()
 
 
 def test_oracle_fewer_than_k_fails():
