@@ -123,5 +123,66 @@ class RsFnt {
     qi_plan* plan_ = nullptr;
 };
 
+// RS-NF4 (src/fec_rs_nf4.h:46-334, src/gf_nf4.h).  A word of word_size bytes
+// packs gf_n = word_size / 2 GF(65537) components that are coded
+// independently with RS-FNT's root and transform (NF4::get_nth_root
+// replicates the prime-field root, gf_nf4.h:450-455; Radix2 as RsFnt,
+// fec_rs_nf4.h:78-96).  So every 16-bit lane of the byte stream is one
+// RS-FNT codeword and the device path is RS-FNT's.  Non-systematic only.
+// OOR marks are (word offset, component bitmask) pairs (NF4::unpack,
+// gf_nf4.h:391-446; restored by NF4::pack(a, flag), :372-383).  word_size 2,
+// 4 or 8: the reference benchmark's T = uint32 / uint64 / __uint128_t
+// (benchmark/benchmark.cpp:283-306, 696-718).
+class RsNf4 {
+  public:
+    // throws std::invalid_argument (bad parameters / word_size) or
+    // std::runtime_error (no HIP device)
+    RsNf4(unsigned word_size, unsigned n_data, unsigned n_parities,
+          size_t pkt_size = 8);
+    RsNf4(const RsNf4&) = delete;
+    RsNf4& operator=(const RsNf4&) = delete;
+
+    unsigned word_size, n_data, n_parities, code_len, n_outputs, gf_n;
+    size_t pkt_size, buf_size;
+    unsigned n;
+
+    int get_n_outputs() const { return static_cast<int>(n); }  // :115-118
+
+    // only whole words are coded (block_size = bytes / word_size,
+    // src/fec_base.h:1083); trailing bytes of a partial word are untouched
+    void encode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
+                                std::vector<uint8_t*>& parities_bufs,
+                                std::vector<Properties>& parities_props,
+                                std::vector<bool>& wanted_idxs,
+                                size_t block_size_bytes);
+    bool decode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
+                                std::vector<uint8_t*>& parities_bufs,
+                                std::vector<Properties>& parities_props,
+                                std::vector<int>& missing_idxs,
+                                std::vector<bool>& wanted_idxs,
+                                size_t block_size_bytes);
+    void encode_streams_vertical(
+        const std::vector<std::istream*>& input_data_bufs,
+        std::vector<std::ostream*>& output_parities_bufs,
+        std::vector<Properties>& output_parities_props);
+    bool decode_streams_vertical(
+        const std::vector<std::istream*>& input_data_bufs,
+        const std::vector<std::istream*>& input_parities_bufs,
+        std::vector<Properties>& input_parities_props,
+        std::vector<std::ostream*>& output_data_bufs);
+
+    const RsFnt& lanes() const { return lanes_; }
+
+  private:
+    RsFnt lanes_;  // the 16-bit lane code (RsFnt NON_SYSTEMATIC, word_size 2)
+};
+
+// (16-bit lane, OOR_MARK) marks <-> (word, component mask) marks of gf_n
+// lanes per word; lane marks must be ascending (as the encoders emit them)
+void nf4_marks_from_lanes(const Properties& lanes, unsigned gf_n,
+                          Properties& words);
+void nf4_marks_to_lanes(const Properties& words, unsigned gf_n,
+                        Properties& lanes);
+
 }  // namespace fec
 }  // namespace qi

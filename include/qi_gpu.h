@@ -136,6 +136,27 @@ int qi_fec_decode_blocks(qi_fec* f, uint8_t** data, uint8_t** parities,
                          uint32_t oor_cap, const int* missing,
                          const int* wanted, size_t block_bytes);
 
+/* ---- RS-NF4 block API (C view of qi::fec::RsNf4; RsNf4<T>,
+ * src/fec_rs_nf4.h:46-334).  word_size 2, 4 or 8 (NULL otherwise): every
+ * word packs word_size/2 GF(65537) components, each coded like an RS-FNT
+ * column on the device.  Non-systematic: n_outputs = k + m.  OOR marks per
+ * output: ascending word offsets in `oor` with the component bitmask in
+ * `flags` (oor_cap entries each, counts exact).  Whole words only. */
+typedef struct qi_nf4 qi_nf4;
+qi_nf4* qi_nf4_new(int word_size, int k, int m);
+void qi_nf4_delete(qi_nf4* f);
+int qi_nf4_n_outputs(const qi_nf4* f);
+/* 0 or -1 */
+int qi_nf4_encode_blocks(qi_nf4* f, uint8_t** data, uint8_t** outputs,
+                         size_t block_bytes, uint32_t* oor, uint32_t* flags,
+                         uint32_t* oor_count, uint32_t oor_cap);
+/* missing: k + m flags.  1 decoded, 0 fewer than k fragments, -1 error */
+int qi_nf4_decode_blocks(qi_nf4* f, uint8_t** data, uint8_t** parities,
+                         const uint32_t* oor, const uint32_t* flags,
+                         const uint32_t* oor_count, uint32_t oor_cap,
+                         const int* missing, const int* wanted,
+                         size_t block_bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,12 @@ def _declare(lib):
         "qi_fec_n_outputs": (I, [V]),
         "qi_fec_encode_blocks": (I, [V, c_u8pp, c_u8pp, SZ, V, V, U32]),
         "qi_fec_decode_blocks": (I, [V, c_u8pp, c_u8pp, V, V, U32, V, V, SZ]),
+        "qi_nf4_new": (V, [I, I, I]),
+        "qi_nf4_delete": (None, [V]),
+        "qi_nf4_n_outputs": (I, [V]),
+        "qi_nf4_encode_blocks": (I, [V, c_u8pp, c_u8pp, SZ, V, V, V, U32]),
+        "qi_nf4_decode_blocks": (I, [V, c_u8pp, c_u8pp, V, V, V, U32, V, V,
+                                     SZ]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -227,6 +233,51 @@ class Fec:
     def close(self):
         if self.h:
             lib().qi_fec_delete(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Nf4:
+    """RS-NF4 block API (qi::fec::RsNf4 via the qi_nf4_* C view)."""
+
+    def __init__(self, word_size, k, m):
+        require_device()
+        self.ws, self.k, self.m = word_size, k, m
+        self.h = lib().qi_nf4_new(word_size, k, m)
+        if not self.h:
+            raise ValueError(f"qi_nf4_new({word_size}, {k}, {m}) failed")
+        self.n_outputs = lib().qi_nf4_n_outputs(self.h)
+
+    def encode(self, data, outputs, oor, flags, counts):
+        """data: k uint8 rows; outputs: n_outputs rows (None = unwanted);
+        oor/flags: (n_outputs, cap) uint32; counts: (n_outputs,) uint32."""
+        rc = lib().qi_nf4_encode_blocks(
+            self.h, ptr_array(data), ptr_array(outputs), len(data[0]),
+            oor.ctypes.data_as(C.c_void_p), flags.ctypes.data_as(C.c_void_p),
+            counts.ctypes.data_as(C.c_void_p), oor.shape[1])
+        if rc:
+            raise RuntimeError(f"qi_nf4_encode_blocks failed: {rc}")
+
+    def decode(self, data, parities, oor, flags, counts, missing, wanted):
+        """Returns 1 (decoded) or 0 (fewer than k fragments)."""
+        rc = lib().qi_nf4_decode_blocks(
+            self.h, ptr_array(data), ptr_array(parities),
+            oor.ctypes.data_as(C.c_void_p), flags.ctypes.data_as(C.c_void_p),
+            counts.ctypes.data_as(C.c_void_p), oor.shape[1],
+            missing.ctypes.data_as(C.c_void_p),
+            wanted.ctypes.data_as(C.c_void_p), len(data[0]))
+        if rc < 0:
+            raise RuntimeError(f"qi_nf4_decode_blocks failed: {rc}")
+        return rc
+
+    def close(self):
+        if self.h:
+            lib().qi_nf4_delete(self.h)
             self.h = None
 
     def __del__(self):

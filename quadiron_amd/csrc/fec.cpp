@@ -523,6 +523,115 @@ bool RsFnt::decode_streams_vertical(
     return true;
 }
 
+// ----------------------------------------------------------------- RS-NF4
+
+void nf4_marks_from_lanes(const Properties& lanes, unsigned g,
+                          Properties& words)
+{
+    // encode_post_process (src/fec_rs_nf4.h:271-289): one mark per word,
+    // bit c set when component c was 65536 (NF4::unpack, gf_nf4.h:421-446)
+    words.clear();
+    size_t cur = 0;
+    uint32_t mask = 0;
+    for (auto const& it : lanes.get_map()) {
+        const size_t w = it.first / g;
+        if (mask && w != cur) {
+            words.add(cur, mask);
+            mask = 0;
+        }
+        cur = w;
+        mask |= 1u << (it.first % g);
+    }
+    if (mask)
+        words.add(cur, mask);
+}
+
+void nf4_marks_to_lanes(const Properties& words, unsigned g, Properties& lanes)
+{
+    // decode_prepare (src/fec_rs_nf4.h:291-317): NF4::pack(a, flag) sets the
+    // flagged components to 65536 (gf_nf4.h:372-383)
+    lanes.clear();
+    for (auto const& it : words.get_map())
+        for (unsigned c = 0; c < g; c++)
+            if ((it.second >> c) & 1u)
+                lanes.add(it.first * g + c, OOR_MARK);
+}
+
+namespace {
+
+unsigned nf4_word_size(unsigned ws)
+{
+    if (ws != 2 && ws != 4 && ws != 8)
+        throw std::invalid_argument("RsNf4: word_size must be 2, 4 or 8");
+    return ws;
+}
+
+}  // namespace
+
+RsNf4::RsNf4(unsigned ws, unsigned k, unsigned m, size_t pkt)
+    : word_size(nf4_word_size(ws)), n_data(k), n_parities(m), code_len(k + m),
+      n_outputs(k + m), gf_n(ws / 2), pkt_size(pkt), buf_size(pkt * ws), n(0),
+      lanes_(FecType::NON_SYSTEMATIC, 2, k, m, pkt * (ws / 2))
+{
+    n = lanes_.n;
+}
+
+void RsNf4::encode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
+                                   std::vector<uint8_t*>& parities_bufs,
+                                   std::vector<Properties>& parities_props,
+                                   std::vector<bool>& wanted_idxs,
+                                   size_t block_size_bytes)
+{
+    std::vector<Properties> lp(n_outputs);
+    lanes_.encode_blocks_vertical(data_bufs, parities_bufs, lp, wanted_idxs,
+                                  block_size_bytes / word_size * word_size);
+    for (unsigned i = 0; i < n_outputs; i++)
+        nf4_marks_from_lanes(lp[i], gf_n, parities_props[i]);
+}
+
+bool RsNf4::decode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
+                                   std::vector<uint8_t*>& parities_bufs,
+                                   std::vector<Properties>& parities_props,
+                                   std::vector<int>& missing_idxs,
+                                   std::vector<bool>& wanted_idxs,
+                                   size_t block_size_bytes)
+{
+    std::vector<Properties> lp(n_outputs);
+    for (unsigned i = 0; i < n_outputs; i++) {
+        parities_props[i].sort();  // as DecodeContext (src/fec_context.h:93-97)
+        nf4_marks_to_lanes(parities_props[i], gf_n, lp[i]);
+    }
+    return lanes_.decode_blocks_vertical(data_bufs, parities_bufs, lp,
+                                         missing_idxs, wanted_idxs,
+                                         block_size_bytes / word_size * word_size);
+}
+
+void RsNf4::encode_streams_vertical(
+    const std::vector<std::istream*>& input_data_bufs,
+    std::vector<std::ostream*>& output_parities_bufs,
+    std::vector<Properties>& output_parities_props)
+{
+    std::vector<Properties> lp(n_outputs);
+    lanes_.encode_streams_vertical(input_data_bufs, output_parities_bufs, lp);
+    for (unsigned i = 0; i < n_outputs; i++)
+        nf4_marks_from_lanes(lp[i], gf_n, output_parities_props[i]);
+}
+
+bool RsNf4::decode_streams_vertical(
+    const std::vector<std::istream*>& input_data_bufs,
+    const std::vector<std::istream*>& input_parities_bufs,
+    std::vector<Properties>& input_parities_props,
+    std::vector<std::ostream*>& output_data_bufs)
+{
+    std::vector<Properties> lp(n_outputs);
+    for (unsigned i = 0; i < n_outputs; i++) {
+        input_parities_props[i].sort();
+        nf4_marks_to_lanes(input_parities_props[i], gf_n, lp[i]);
+    }
+    return lanes_.decode_streams_vertical(input_data_bufs, input_parities_bufs,
+                                          lp, output_data_bufs);
+}
+
 }  // namespace fec
 }  // namespace qi
 
@@ -604,6 +713,106 @@ int qi_fec_decode_blocks(qi_fec* h, uint8_t** data, uint8_t** parities,
             const uint32_t c = oor_count[i] < cap ? oor_count[i] : cap;
             for (uint32_t e = 0; e < c; e++)
                 props[i].add(oor[static_cast<size_t>(i) * cap + e], qi::OOR_MARK);
+        }
+        std::vector<int> miss(missing, missing + f.code_len);
+        std::vector<bool> want(f.n_data);
+        for (unsigned i = 0; i < f.n_data; i++)
+            want[i] = wanted[i] != 0;
+        return f.decode_blocks_vertical(dv, pv, props, miss, want, block_bytes) ? 1
+                                                                                : 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
+}  // extern "C"
+
+struct qi_nf4 {
+    qi::fec::RsNf4* f;
+};
+
+extern "C" {
+
+qi_nf4* qi_nf4_new(int word_size, int k, int m)
+{
+    try {
+        if (word_size < 0 || k < 1 || m < 1)
+            return nullptr;
+        auto* h = new qi_nf4;
+        try {
+            h->f = new qi::fec::RsNf4(static_cast<unsigned>(word_size),
+                                      static_cast<unsigned>(k),
+                                      static_cast<unsigned>(m), 1024);
+        } catch (...) {
+            delete h;
+            return nullptr;
+        }
+        return h;
+    } catch (...) {
+        return nullptr;
+    }
+}
+
+void qi_nf4_delete(qi_nf4* h)
+{
+    if (h) {
+        delete h->f;
+        delete h;
+    }
+}
+
+int qi_nf4_n_outputs(const qi_nf4* h)
+{
+    return h ? static_cast<int>(h->f->n_outputs) : -1;
+}
+
+int qi_nf4_encode_blocks(qi_nf4* h, uint8_t** data, uint8_t** outputs,
+                         size_t block_bytes, uint32_t* oor, uint32_t* flags,
+                         uint32_t* oor_count, uint32_t cap)
+{
+    try {
+        qi::fec::RsNf4& f = *h->f;
+        std::vector<uint8_t*> dv(data, data + f.n_data);
+        std::vector<uint8_t*> pv(outputs, outputs + f.n_outputs);
+        std::vector<qi::Properties> props(f.n_outputs);
+        std::vector<bool> wanted(f.n_outputs);
+        for (unsigned i = 0; i < f.n_outputs; i++)
+            wanted[i] = outputs[i] != nullptr;
+        f.encode_blocks_vertical(dv, pv, props, wanted, block_bytes);
+        for (unsigned i = 0; i < f.n_outputs; i++) {
+            uint32_t c = 0;
+            for (auto const& it : props[i].get_map()) {
+                if (c < cap) {
+                    oor[static_cast<size_t>(i) * cap + c] =
+                        static_cast<uint32_t>(it.first);
+                    flags[static_cast<size_t>(i) * cap + c] = it.second;
+                }
+                c++;
+            }
+            oor_count[i] = c;
+        }
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
+int qi_nf4_decode_blocks(qi_nf4* h, uint8_t** data, uint8_t** parities,
+                         const uint32_t* oor, const uint32_t* flags,
+                         const uint32_t* oor_count, uint32_t cap,
+                         const int* missing, const int* wanted,
+                         size_t block_bytes)
+{
+    try {
+        qi::fec::RsNf4& f = *h->f;
+        std::vector<uint8_t*> dv(data, data + f.n_data);
+        std::vector<uint8_t*> pv(parities, parities + f.n_outputs);
+        std::vector<qi::Properties> props(f.n_outputs);
+        for (unsigned i = 0; i < f.n_outputs; i++) {
+            const uint32_t c = oor_count[i] < cap ? oor_count[i] : cap;
+            for (uint32_t e = 0; e < c; e++)
+                props[i].add(oor[static_cast<size_t>(i) * cap + e],
+                             flags[static_cast<size_t>(i) * cap + e]);
         }
         std::vector<int> miss(missing, missing + f.code_len);
         std::vector<bool> want(f.n_data);
