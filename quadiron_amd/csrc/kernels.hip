@@ -89,6 +89,13 @@ struct Region {
 #endif
 constexpr int kAuxLd = QI_AUX_LD;
 constexpr int kAuxSt = QI_AUX_ST;
+// the matrix-core kernel's stores cover a 128-byte line in two 16-byte
+// halves per lane group: default policy, so the L2 merges them into whole
+// lines (streaming nt|sc1 stores would reach HBM as partial lines)
+#ifndef QI_MFMA_AUX_ST
+#define QI_MFMA_AUX_ST 0
+#endif
+constexpr int kAuxStMf = QI_MFMA_AUX_ST;
 
 // XCD-aware block -> (stripe, tile) map.  Workgroups are dispatched
 // round-robin over the 8 XCDs (block b runs on XCD b % 8), so with the plain
@@ -476,9 +483,12 @@ encode_fnt_kernel(
 constexpr int kMaxTileOor = 256;
 typedef short qi_short2 __attribute__((ext_vector_type(2)));
 
-// byte extents of the stripe regions a matrix launch touches
+// launch geometry of a matrix kernel: byte extents of the stripe regions it
+// touches and its first column (a tail launch starts past the columns the
+// matrix-core kernel covered)
 struct MatExt {
     uint32_t e0, e1, eo;
+    long long c0;
 };
 
 template <int KP, int COLS, bool FULL, bool BUF>
@@ -630,7 +640,7 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
     int s, tile;
     block_map(blockIdx.x, tiles, s, tile);
     const int kin = L.kin;
-    const long long col0 = static_cast<long long>(tile) * kBlock * COLS;
+    const long long col0 = ext.c0 + static_cast<long long>(tile) * kBlock * COLS;
     const long long col1 = col0 + kBlock * COLS;
     const long long col = col0 + static_cast<long long>(threadIdx.x) * COLS;
     const uint32_t voff = static_cast<uint32_t>(col * 2);
@@ -727,6 +737,309 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
         matrix_compute<KP, COLS, false, BUF>(L, M, xp, go, ors, voff, col, col0,
                                              words - col, s, n_rm, rm, n_lm, s_i,
                                              s_col, out_oor);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Matrix apply on the matrix cores (v_mfma_i32_16x16x32_i8), kin <= 64.
+//
+// The product of matrix_kernel, out[t] = sum_i M[t][i] x_i mod q, with the
+// u16 inputs and the row-scaled coefficients split into signed bytes:
+//   x = 256 h' + l' + 32896        h' = (x >> 8) - 128, l' = (x & 255) - 128
+//   c = 256 a + b                  a, b in [-128, 127] (split_i8)
+// and 2^16 = -1 (mod q):
+//   sum_i c x = 256 D2 + D1 - D0 + 32896 sum_i c
+//   D0 = sum a h',  D1 = sum b l',  D2 = sum b h' + a l'
+// -- three int8 GEMMs over K = [h' rows ; l' rows] against the per-stripe
+// operand tiles [a|0], [0|b], [b|a] (matrix_pack.h pack_mf_dword; D1 starts
+// at kmf[t] = 32896 sum c).  |D| < 2^21 for kin <= 64, so the int32
+// accumulators and the epilogue never overflow.  The dot2 kernel's ~19 VALU
+// per (output, column) become ~5 of epilogue, so the decode is HBM-bound
+// rather than VALU-bound.
+//
+// Orientation D^T = X^T M^T: the A operand is the tile's byte planes,
+// staged in LDS and read with ds_read_b64_tr_b8 (lane 2q+p of a 16-lane
+// group addresses row q, bytes 8p..8p+7 of an 8 x 16-byte block; lane i gets
+// column i -- profiles/r1_mfma_probe.txt); the B operand is the coefficient
+// tile, pre-swizzled in lane order.  A lane's 4 results are 4 adjacent LDS
+// columns of ONE output row t = lane & 15.  The LDS image stores column
+// u = 16 g + 4 T + j of every 64-column super tile at byte 4 g + j of 16-byte
+// chunk T, so after the 4 chunks of a super tile lane (g, t) holds the 16
+// contiguous columns 16 g .. 16 g + 15 of row t: two b128 stores.
+// Whole kRouteTile column tiles only; launch_matrix sends the tail to
+// matrix_kernel.
+// ---------------------------------------------------------------------------
+typedef int qi_v4i __attribute__((ext_vector_type(4)));
+typedef int qi_v2i __attribute__((ext_vector_type(2)));
+typedef unsigned int qi_v4u __attribute__((ext_vector_type(4)));
+
+template <int KS, int COLS>
+struct MfmaTile {
+    static constexpr int kCols = kBlock * COLS;  // columns per block
+    static constexpr int kRows = 16 * KS;        // rows per byte plane
+    static constexpr int kPitch = kCols + 16;    // LDS row pitch: +4 banks/row
+    static constexpr size_t kImg = static_cast<size_t>(2 * kRows) * kPitch;
+    // image + OOR scan scratch (s_i, s_col) + s_cnt
+    static constexpr size_t kLds = kImg + 2 * 4 * kMaxTileOor + 16;
+};
+
+template <int KS, int COLS>
+__global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
+    MatLayout L, const int32_t* __restrict__ mat, long long mat_stride,
+    const int32_t* __restrict__ ids, long long ids_stride, RowSrc src,
+    RowDst dst, MatExt ext, long long words, int tiles, Oor in_oor,
+    int slot_base, Oor out_oor, const uint32_t* __restrict__ route,
+    long long route_stride, uint32_t* err)
+{
+    using G = MfmaTile<KS, COLS>;
+    constexpr int NCOL = G::kCols, KH = G::kRows, RSB = G::kPitch;
+    // one dynamic region (16-byte aligned base: no static LDS in front)
+    extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
+    uint8_t* img = qi_lds;
+    int* s_i = reinterpret_cast<int*>(qi_lds + G::kImg);
+    uint32_t* s_col = reinterpret_cast<uint32_t*>(s_i + kMaxTileOor);
+    int* s_cnt = reinterpret_cast<int*>(s_col + kMaxTileOor);
+
+    int s, tile;
+    block_map(blockIdx.x, tiles, s, tile);
+    const int kin = L.kin;
+    const long long col0 = static_cast<long long>(tile) * NCOL;
+    const long long col1 = col0 + NCOL;
+    const uint32_t cl = threadIdx.x * COLS;  // this thread's first column
+    const uint32_t voff = static_cast<uint32_t>((col0 + cl) * 2);
+    const int32_t* M = mat + s * mat_stride;
+    const int32_t* sid = ids ? ids + s * ids_stride : nullptr;
+    const Region<true> g0(src.base0 + s * src.ss0, ext.e0);
+    const Region<true> g1(src.base1 ? src.base1 + s * src.ss1 : src.base0,
+                          ext.e1);
+    const Region<true> go(dst.base + s * dst.ss, ext.eo);
+
+    // OOR marks of the received rows in this tile: route table (scalar
+    // loads) or bucket scan, as matrix_kernel
+    int n_rm = 0;
+    const uint32_t* rm = nullptr;
+    bool scan = in_oor.counts != nullptr;
+    if (route) {
+        const uint32_t* rt =
+            route + s * route_stride + (col0 / kRouteTile) * kRouteStride;
+        const uint32_t rc = rt[0];
+        if (rc <= static_cast<uint32_t>(kRouteCap)) {
+            n_rm = static_cast<int>(rc);
+            rm = rt + 1;
+            scan = false;
+        }
+    }
+
+    // operand tiles of output block 0 (per-lane loads; issued before the row
+    // loads so their latency hides behind the staging)
+    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int g = l >> 4, q = (l & 15) >> 1, p = l & 1, tl = l & 15;
+    const int RB = L.RB();
+    const int32_t* mf = M + L.mf();
+    const int32_t* kmf = M + L.kmf();
+    const int32_t* rscale = M + L.rscale();
+    const int32_t* plain = M + L.plain();
+    auto load_ops = [&](int rb, qi_v2i (&b)[KS][3], int32_t& kt, int32_t& rs) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++)
+#pragma unroll
+            for (int ty = 0; ty < 3; ty++)
+                b[ks][ty] = *reinterpret_cast<const qi_v2i*>(
+                    mf + ((rb * KS + ks) * 3 + ty) * 128 + l * 2);
+        const int t = 16 * rb + tl;
+        kt = t < L.R ? kmf[t] : 0;
+        rs = t < L.R ? rscale[t] : 1;
+    };
+    qi_v2i bop[KS][3];
+    int32_t kt, rs;
+    load_ops(0, bop, kt, rs);
+
+    // stage the tile as byte planes h' (rows 0..KH-1) and l' (rows KH..),
+    // all row loads issued back to back; rows past kin load a clamped row
+    // (their operand bytes are 0)
+    uint32_t w[KH][COLS / 2];
+#pragma unroll
+    for (int i = 0; i < KH; i++) {
+        const int ii = i < kin ? i : kin - 1;
+        const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
+        const bool lo = id < src.split;
+        Region<true> g = g0;
+        g.r = lo ? g0.r : g1.r;
+        const uint32_t off = static_cast<uint32_t>(
+            lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
+        ld_dw<COLS / 2, true, kAuxLd>(g, off, voff, w[i]);
+    }
+    const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) +
+                          4 * ((cl % 64) / 16) + cl % 4;
+#pragma unroll
+    for (int i = 0; i < KH; i++) {
+        if constexpr (COLS == 4) {
+            // [c0 lo, c0 hi, c1 lo, c1 hi] [c2 lo, ...] -> hi / lo planes
+            const uint32_t hi =
+                __builtin_amdgcn_perm(w[i][1], w[i][0], 0x07050301u) ^ 0x80808080u;
+            const uint32_t lo =
+                __builtin_amdgcn_perm(w[i][1], w[i][0], 0x06040200u) ^ 0x80808080u;
+            *reinterpret_cast<uint32_t*>(img + i * RSB + lpos) = hi;
+            *reinterpret_cast<uint32_t*>(img + (KH + i) * RSB + lpos) = lo;
+        } else {
+            const uint32_t hi =
+                __builtin_amdgcn_perm(0u, w[i][0], 0x0c0c0301u) ^ 0x8080u;
+            const uint32_t lo =
+                __builtin_amdgcn_perm(0u, w[i][0], 0x0c0c0200u) ^ 0x8080u;
+            *reinterpret_cast<uint16_t*>(img + i * RSB + lpos) =
+                static_cast<uint16_t>(hi);
+            *reinterpret_cast<uint16_t*>(img + (KH + i) * RSB + lpos) =
+                static_cast<uint16_t>(lo);
+        }
+    }
+    int n_lm = 0;
+    if (scan) {  // block-uniform
+        if (threadIdx.x == 0)
+            *s_cnt = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < kin; i += kBlock) {
+            const int id = sid ? sid[i] : i;
+            const int slot = (src.by_pos ? i : id) - slot_base;
+            if (slot < 0)
+                continue;
+            const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
+            uint32_t c = in_oor.counts[bk];
+            if (c > static_cast<uint32_t>(in_oor.cap))
+                c = in_oor.cap;
+            for (uint32_t e = 0; e < c; e++) {
+                const uint32_t wc = in_oor.entries[bk * in_oor.cap + e];
+                if (wc >= col0 && wc < col1 && wc < words) {
+                    const int p = atomicAdd(s_cnt, 1);
+                    if (p < kMaxTileOor) {
+                        s_i[p] = i;
+                        s_col[p] = wc;
+                    } else {
+                        atomicOr(err, 1u);
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (scan)
+        n_lm = min(*s_cnt, kMaxTileOor);
+
+    // matrix cores: wave wv covers COLS super tiles of 64 columns, for each
+    // block of 16 output rows in turn (the next block's operands prefetched)
+    const bool rec = out_oor.counts != nullptr;
+    const long long rbase = col0 / kRouteTile * kRouteTile;
+    const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
+    // generic -> LDS address space (C-style cast: reinterpret_cast cannot
+    // change the address space)
+    auto* lds = (__attribute__((address_space(3))) uint8_t*)img;
+    const uint32_t abase = static_cast<uint32_t>((8 * g + q) * RSB + 8 * p);
+    for (int rb = 0; rb < RB; rb++) {
+        const int t = 16 * rb + tl;
+        const bool trow = t < L.R;
+        qi_v2i bnx[KS][3];
+        int32_t ktn = 0, rsn = 1;
+        if (rb + 1 < RB)
+            load_ops(rb + 1, bnx, ktn, rsn);
+        for (int st = 0; st < COLS; st++) {
+            const int ST = wv * COLS + st;
+            qi_v4i acc[4][3];
+#pragma unroll
+            for (int T = 0; T < 4; T++) {
+                acc[T][0] = qi_v4i{0, 0, 0, 0};
+                acc[T][1] = qi_v4i{kt, kt, kt, kt};
+                acc[T][2] = qi_v4i{0, 0, 0, 0};
+#pragma unroll
+                for (int ks = 0; ks < KS; ks++) {
+                    auto* pa = (__attribute__((address_space(3))) qi_v2i*)(
+                        lds + abase + 32 * ks * RSB + (4 * ST + T) * 16);
+                    const long a = __builtin_bit_cast(
+                        long, __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa));
+#pragma unroll
+                    for (int ty = 0; ty < 3; ty++)
+                        acc[T][ty] = __builtin_amdgcn_mfma_i32_16x16x32_i8(
+                            a, __builtin_bit_cast(long, bop[ks][ty]), acc[T][ty], 0,
+                            0, 0);
+                }
+            }
+            // epilogue: lane (g, t) holds row t, columns cb .. cb + 15;
+            // result j of chunk T is LDS byte 4 g + j = column 16 g + 4 T + j
+            const long long cb = col0 + 64 * ST + 16 * g;
+            int32_t y[16];
+#pragma unroll
+            for (int T = 0; T < 4; T++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    y[4 * T + j] = fold(fold((acc[T][2][j] << 8) + acc[T][1][j] -
+                                             acc[T][0][j]));
+            // restored OOR symbols of the received rows: 65536 == -1 where
+            // the stored word is 0 (decode_prepare, src/fec_base.h:1361-1404)
+            for (int e = 0; e < n_rm + n_lm; e++) {
+                long long wc;
+                int pos;
+                if (e < n_rm) {
+                    const uint32_t v = rm[e];
+                    pos = static_cast<int>(v >> 16);
+                    wc = rbase + (v & 0xffffu);
+                } else {
+                    pos = s_i[e - n_rm];
+                    wc = s_col[e - n_rm];
+                }
+                const long long d = wc - cb;
+                if (trow && d >= 0 && d < 16) {
+                    const int32_t corr = plain[t * kin + pos];
+#pragma unroll
+                    for (int c = 0; c < 16; c++)
+                        if (c == d)
+                            y[c] = fold(fold(y[c] - corr));
+                }
+            }
+            if (__builtin_amdgcn_ballot_w64(rs != 1)) {
+#pragma unroll
+                for (int c = 0; c < 16; c++)
+                    if (rs != 1)
+                        y[c] = fold(fold(mul_i24_s(y[c], rs)));
+            }
+            uint32_t bad = 0;
+#pragma unroll
+            for (int c = 0; c < 16; c++)
+                bad |= static_cast<uint32_t>(y[c]);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64((bad >> 16) != 0) != 0, 0)) {
+#pragma unroll
+                for (int c = 0; c < 16; c++) {
+                    if (static_cast<uint32_t>(y[c]) > 65535u) {
+                        if (rec && trow)
+                            record_oor(out_oor, s, t, cb + c);
+                        y[c] = 0;  // 65536 (or its alias -1) is stored as 0
+                    }
+                }
+            }
+            if (trow) {
+                qi_v4u o0, o1;
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    o0[c] = pack_lo(static_cast<uint32_t>(y[2 * c]),
+                                    static_cast<uint32_t>(y[2 * c + 1]));
+                    o1[c] = pack_lo(static_cast<uint32_t>(y[8 + 2 * c]),
+                                    static_cast<uint32_t>(y[8 + 2 * c + 1]));
+                }
+                const uint32_t vo = static_cast<uint32_t>(t) * ors +
+                                    static_cast<uint32_t>(cb * 2);
+                __builtin_amdgcn_raw_buffer_store_b128(o0, go.r, static_cast<int>(vo),
+                                                       0, kAuxStMf);
+                __builtin_amdgcn_raw_buffer_store_b128(o1, go.r,
+                                                       static_cast<int>(vo + 16), 0,
+                                                       kAuxStMf);
+            }
+        }
+        if (rb + 1 < RB) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++)
+#pragma unroll
+                for (int ty = 0; ty < 3; ty++)
+                    bop[ks][ty] = bnx[ks][ty];
+            kt = ktn;
+            rs = rsn;
+        }
     }
 }
 
@@ -860,7 +1173,14 @@ __global__ __launch_bounds__(64) void decode_ctx_kernel(
     }
     __syncthreads();
     for (int t = tid; t < L.R; t += 64)
-        pack_row(Mt + t * k, k, L.KP, L.R, t, mat);
+        pack_row(Mt + t * k, L, t, mat);
+    if (L.KS()) {
+        // the matrix-core operand tiles, from the `plain` rows just written
+        __threadfence_block();
+        __syncthreads();
+        for (size_t d = tid; d < L.mf_words(); d += 64)
+            mat[L.mf() + d] = pack_mf_dword(L, mat, d);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -992,7 +1312,7 @@ static int mat_launch(const MatLayout& L, const int32_t* mat, long long ms,
                       uint32_t* err, hipStream_t st)
 {
     int tiles;
-    if (grid_for(words, COLS, S, &tiles))
+    if (grid_for(words - ext.c0, COLS, S, &tiles))
         return -1;
     hipLaunchKernelGGL((matrix_kernel<KP, COLS, BUF>), dim3(tiles * S),
                        dim3(kBlock), 0, st, L, mat, ms, ids, is, src, dst, ext,
@@ -1030,6 +1350,42 @@ static int mat_dispatch(int cols, const MatLayout& L, const int32_t* mat,
                                    io, slot_base, oo, route, rstride, err, st);
 }
 
+#ifndef QI_MFMA
+#define QI_MFMA 1
+#endif
+// columns per thread of the KS = 1 matrix-core kernel (4: 1024-column
+// blocks, 35 KB LDS; 2: 512-column blocks, 19 KB LDS, more blocks per CU)
+#ifndef QI_MFMA_COLS1
+#define QI_MFMA_COLS1 4
+#endif
+
+template <int KS, int COLS>
+static int mfma_launch(const MatLayout& L, const int32_t* mat, long long ms,
+                       const int32_t* ids, long long is, RowSrc src, RowDst dst,
+                       MatExt ext, long long words, long long wfull, int S,
+                       Oor io, int slot_base, Oor oo, const uint32_t* route,
+                       long long rstride, uint32_t* err, hipStream_t st)
+{
+    using G = MfmaTile<KS, COLS>;
+    const long long t = wfull / G::kCols;
+    if (t <= 0 || t * S > 0x7fffffffLL)
+        return -1;
+    static bool attr = false;  // dynamic LDS above 64 KiB needs opting in
+    if (G::kLds > 65536 && !attr) {
+        if (hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&matrix_mfma_kernel<KS, COLS>),
+                hipFuncAttributeMaxDynamicSharedMemorySize,
+                static_cast<int>(G::kLds)) != hipSuccess)
+            return -2;
+        attr = true;
+    }
+    hipLaunchKernelGGL((matrix_mfma_kernel<KS, COLS>), dim3(t * S), dim3(kBlock),
+                       G::kLds, st, L, mat, ms, ids, is, src, dst, ext, words,
+                       static_cast<int>(t), io, slot_base, oo, route, rstride,
+                       err);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
                   const int32_t* ids, long long is, RowSrc src, RowDst dst,
                   long long words,
@@ -1048,7 +1404,7 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
         return -4;
     MatExt ext{extent(src.rows0, src.rs0, words),
                extent(src.rows1, src.rs1, words),
-               extent(L.R, dst.rs, words)};
+               extent(L.R, dst.rs, words), 0};
     const bool buf = ext.e0 && ext.eo && (!src.base1 || ext.e1);
     const bool a4 = a2 &&
                     aligned_for(4, src.base0, src.ss0, src.rs0, dst.ss, dst.rs) &&
@@ -1056,6 +1412,24 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
                      aligned_for(4, src.base1, src.ss1, src.rs1, 0, 0)) &&
                     (reinterpret_cast<uintptr_t>(dst.base) % 8) == 0;
     const int cols = !buf ? 1 : a4 ? 4 : a2 ? 2 : 1;
+    // whole kRouteTile column tiles on the matrix cores, the tail (and
+    // everything the MFMA kernel does not take) on the dot2 kernel
+    const long long wfull = words / kRouteTile * kRouteTile;
+    if (QI_MFMA && L.KS() > 0 && buf && a4 && wfull > 0) {
+        int rc;
+        if (L.KS() == 1)
+            rc = mfma_launch<1, QI_MFMA_COLS1>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
+                                   S, io, slot_base, oo, route, rstride, err, st);
+        else if (L.KS() == 2)
+            rc = mfma_launch<2, 2>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
+                                   S, io, slot_base, oo, route, rstride, err, st);
+        else
+            rc = mfma_launch<4, 2>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
+                                   S, io, slot_base, oo, route, rstride, err, st);
+        if (rc || wfull == words)
+            return rc;
+        ext.c0 = wfull;
+    }
     switch (L.KP) {
     case 2:
         return mat_dispatch<2>(cols, L, mat, ms, ids, is, src, dst, ext, words,

@@ -1,25 +1,86 @@
-// Packing of a canonical GF(65537) matrix row into the dot2 form used by the
-// matrix kernel (host + device).  See qi_internal.h MatLayout.
+// Packing of a canonical GF(65537) matrix into the forms the matrix kernels
+// read (host + device): the int16-pair rows of the dot2 kernel
+// (matrix_kernel) and the i8 operand tiles of the matrix-core kernel
+// (matrix_mfma_kernel).
 #pragma once
+
+#include <stddef.h>
 
 #include "gf65537.h"
 
 namespace qi {
+
+// Packed matrix block, one per stripe (decode contexts) or shared (plan):
+//   packed[R][KP]  int16 pairs (balanced, |c| <= 32766) of the row-scaled
+//                  matrix, zero padded past kin
+//   kcorr[R]       32768 * sum_i c[t][i] mod q (undoes the x - 32768 offset)
+//   rscale[R]      balanced inverse row scale (1 = unscaled)
+//   plain[R][kin]  canonical row-scaled entries (OOR corrections)
+//   mf[RB][KS][3][64][2]  i8 operand tiles of matrix_mfma_kernel (kin <= 64):
+//                  RB = ceil(R / 16) output blocks, KS = K-steps of 32
+//                  bytes, 3 operand types, 64 lanes x 8 bytes (pack_mf_dword)
+//   kmf[R]         32896 * sum_i c[t][i] mod q (undoes the byte offsets)
+// The MFMA section exists (KS() > 0) when matrix_mfma_kernel takes the
+// block: kin <= 64 and more than 16 x 16 products per column.  At 16 x 16
+// (the k = 16 decode) the dot2 kernel is as fast and keeps its streaming
+// stores (A/B on MI355X: decode 1.61 ms dot2 vs 1.65 ms MFMA; the 48 x 16
+// systematic encode 3.60 vs 3.80 ms and the 64 x 64 decode 0.35 vs 0.62 ms
+// favour the matrix cores).
+struct MatLayout {
+    int R, kin, KP;
+    QI_HD int KS() const
+    {
+        if (kin > 64 || R * kin <= 256)
+            return 0;
+        return kin <= 16 ? 1 : kin <= 32 ? 2 : 4;
+    }
+    QI_HD int RB() const { return KS() ? (R + 15) / 16 : 0; }
+    QI_HD size_t packed() const { return 0; }
+    QI_HD size_t kcorr() const { return static_cast<size_t>(R) * KP; }
+    QI_HD size_t rscale() const { return kcorr() + R; }
+    QI_HD size_t plain() const { return rscale() + R; }
+    QI_HD size_t mf() const { return plain() + static_cast<size_t>(R) * kin; }
+    QI_HD size_t mf_words() const
+    {
+        return static_cast<size_t>(RB()) * KS() * 3 * 128;
+    }
+    QI_HD size_t kmf() const { return mf() + mf_words(); }
+    QI_HD size_t words() const { return kmf() + (KS() ? R : 0); }
+};
 
 QI_HD int32_t iabs32(int32_t v)
 {
     return v < 0 ? -v : v;
 }
 
-// Pack row t (kin canonical entries) of an R-row block with KP pairs.
-// v_dot2_i32_i16 accumulates acc + x0*c0 + x1*c1 with x in [-32768, 32767]
-// (inputs offset by -32768) and acc in [-32767, 98303] (after fold): the sum
-// stays below 2^31 iff |c| <= 32766, so rows holding one of the 4 residues
-// {32767, 32768, 32769, 32770} are scaled by a unit s first and the result
-// is multiplied back by s^-1 (also kept within |c| <= 32766).
-QI_HD void pack_row(const uint32_t* row, int kin, int KP, int R, int t,
+// Coefficients both kernels can take: v_dot2_i32_i16 accumulates
+// acc + x0*c0 + x1*c1 with x in [-32768, 32767] (inputs offset by -32768)
+// and acc in [-32767, 98303] (after fold), which stays below 2^31 iff
+// |c| <= 32766; the i8 split c = 256 a + b (split_i8) reaches every
+// balanced residue but 32640.
+QI_HD bool coef_ok(int32_t c)
+{
+    return iabs32(c) <= 32766 && c != 32640;
+}
+
+// c = 256 a + b (mod q) with a, b in [-128, 127], for a canonical c whose
+// balanced form is not 32640 (256 a + b spans [-32896, 32639])
+QI_HD void split_i8(uint32_t c, int32_t& a, int32_t& b)
+{
+    int32_t v = balanced(c);
+    if (v > 32639)
+        v -= kQ;
+    b = ((v + 128) & 255) - 128;
+    a = (v - b) / 256;
+}
+
+// Pack row t (kin canonical entries) of the block.  Rows holding a
+// coefficient that breaks coef_ok are scaled by a unit s first and the
+// result is multiplied back by s^-1 (rscale, also |s^-1| <= 32766).
+QI_HD void pack_row(const uint32_t* row, const MatLayout& L, int t,
                     int32_t* block)
 {
+    const int kin = L.kin, KP = L.KP;
     uint32_t s = 1;
     for (;; s++) {
         const int32_t si = balanced(powmod_c(s, 65535u));
@@ -27,8 +88,7 @@ QI_HD void pack_row(const uint32_t* row, int kin, int KP, int R, int t,
             continue;
         bool ok = true;
         for (int i = 0; i < kin; i++) {
-            const int32_t c = balanced(mulmod_c(row[i], s));
-            if (iabs32(c) > 32766) {
+            if (!coef_ok(balanced(mulmod_c(row[i], s)))) {
                 ok = false;
                 break;
             }
@@ -37,9 +97,7 @@ QI_HD void pack_row(const uint32_t* row, int kin, int KP, int R, int t,
             break;
     }
     int32_t* packed = block + static_cast<size_t>(t) * KP;
-    int32_t* kcorr = block + static_cast<size_t>(R) * KP;
-    int32_t* rscale = kcorr + R;
-    int32_t* plain = rscale + R;
+    int32_t* plain = block + L.plain();
     uint64_t sum = 0;
     for (int j = 0; j < KP; j++) {
         int32_t lo = 0, hi = 0;
@@ -55,8 +113,47 @@ QI_HD void pack_row(const uint32_t* row, int kin, int KP, int R, int t,
         plain[static_cast<size_t>(t) * kin + i] = static_cast<int32_t>(c);
         sum += c;
     }
-    kcorr[t] = static_cast<int32_t>(mulmod_c(static_cast<uint32_t>(sum % 65537u), 32768u));
-    rscale[t] = balanced(powmod_c(s, 65535u));
+    const uint32_t sq = static_cast<uint32_t>(sum % 65537u);
+    block[L.kcorr() + t] = static_cast<int32_t>(mulmod_c(sq, 32768u));
+    block[L.rscale() + t] = balanced(powmod_c(s, 65535u));
+    if (L.KS())
+        block[L.kmf() + t] = static_cast<int32_t>(mulmod_c(sq, 32896u));
+}
+
+// Dword d of the MFMA operand tiles, from the `plain` rows pack_row wrote.
+// Tile (rb, ks, ty) gives lane l = 16 g + (t & 15), t = 16 rb + (t & 15),
+// the B operand bytes B[K][t], K = 32 ks + 8 g + j (j = 0..7 over its two
+// dwords), where K < KH = 16 KS is byte plane h' of input K and K >= KH
+// is plane l' of input K - KH (x = 256 h' + l' + 32896):
+//   ty 0: [a | 0]   ty 1: [0 | b]   ty 2: [b | a]       (c = 256 a + b)
+// i.e. D0 = sum a h', D1 = sum b l', D2 = sum (b h' + a l') and
+// sum c x = 256 D2 + D1 - D0 + 32896 sum c  (2^16 = -1 mod q).
+QI_HD int32_t pack_mf_dword(const MatLayout& L, const int32_t* block, size_t d)
+{
+    const int KS = L.KS(), KH = 16 * KS;
+    const size_t tile = d / 128;
+    const int rem = static_cast<int>(d % 128), lane = rem / 2, dw = rem % 2;
+    const int ty = static_cast<int>(tile % 3);
+    const int ks = static_cast<int>((tile / 3) % static_cast<size_t>(KS));
+    const int rb = static_cast<int>(tile / (3 * static_cast<size_t>(KS)));
+    const int t = 16 * rb + (lane & 15), g = lane >> 4;
+    if (t >= L.R)
+        return 0;
+    const int32_t* plain = block + L.plain() + static_cast<size_t>(t) * L.kin;
+    uint32_t v = 0;
+    for (int jb = 0; jb < 4; jb++) {
+        const int K = 32 * ks + 8 * g + 4 * dw + jb;
+        const bool hp = K < KH;
+        const int i = hp ? K : K - KH;
+        int32_t e = 0;
+        if (i < L.kin) {
+            int32_t a, b;
+            split_i8(static_cast<uint32_t>(plain[i]), a, b);
+            e = ty == 0 ? (hp ? a : 0) : ty == 1 ? (hp ? 0 : b) : (hp ? b : a);
+        }
+        v |= (static_cast<uint32_t>(e) & 0xffu) << (8 * jb);
+    }
+    return static_cast<int32_t>(v);
 }
 
 }  // namespace qi

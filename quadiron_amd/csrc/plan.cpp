@@ -67,7 +67,9 @@ void pack_matrix(const MatLayout& L, const uint32_t* M, int32_t* block)
 {
     std::memset(block, 0, L.words() * sizeof(int32_t));
     for (int t = 0; t < L.R; t++)
-        pack_row(M + static_cast<size_t>(t) * L.kin, L.kin, L.KP, L.R, t, block);
+        pack_row(M + static_cast<size_t>(t) * L.kin, L, t, block);
+    for (size_t d = 0; d < L.mf_words(); d++)
+        block[L.mf() + d] = pack_mf_dword(L, block, d);
 }
 
 }  // namespace qi

@@ -8,22 +8,9 @@
 
 #include <vector>
 
-namespace qi {
+#include "matrix_pack.h"  // MatLayout: the packed matrix block
 
-// Packed interpolation / generator matrix block, one per stripe (or shared).
-//   packed[R][KP]  int16 pairs (balanced, |c| <= 32766) of the row-scaled
-//                  matrix, zero padded past kin
-//   kcorr[R]       32768 * sum_i c[t][i] mod q (undoes the x - 32768 offset)
-//   rscale[R]      balanced inverse row scale (1 = unscaled)
-//   plain[R][kin]  canonical row-scaled entries (OOR corrections)
-struct MatLayout {
-    int R, kin, KP;
-    __host__ __device__ size_t packed() const { return 0; }
-    __host__ __device__ size_t kcorr() const { return static_cast<size_t>(R) * KP; }
-    __host__ __device__ size_t rscale() const { return kcorr() + R; }
-    __host__ __device__ size_t plain() const { return rscale() + R; }
-    __host__ __device__ size_t words() const { return plain() + static_cast<size_t>(R) * kin; }
-};
+namespace qi {
 
 // OOR routing: the decode context keeps, per stripe and per tile of
 // kRouteTile columns, the marks of the received rows that fall in the tile

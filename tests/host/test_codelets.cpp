@@ -6,7 +6,9 @@
 //     int32 overflow aborts under UBSan; 24-bit multiply operands are
 //     asserted in mul_tw via QI_HOST_CHECK),
 //  3. the dot2 matrix path (pack_row + emulated v_dot2_i32_i16) against a
-//     plain matrix-vector product, checking the 32-bit accumulator bound.
+//     plain matrix-vector product, checking the 32-bit accumulator bound,
+//  4. the matrix-core path (pack_mf_dword operand tiles x byte planes, the
+//     three int32 GEMMs of matrix_mfma_kernel and its epilogue) likewise.
 #include <cassert>
 #include <cstdio>
 #include <cstdlib>
@@ -113,11 +115,10 @@ static void test_matrix(std::mt19937_64& g)
             v = mode == 0 ? 32767u + static_cast<uint32_t>(g() % 4)
                           : static_cast<uint32_t>(g() % 65537);
         }
-        std::vector<int32_t> blk(static_cast<size_t>(R) * KP + 2 * R +
-                                 static_cast<size_t>(R) * kin);
+        const MatLayout L{R, kin, KP};
+        std::vector<int32_t> blk(L.words());
         for (int t = 0; t < R; t++)
-            pack_row(M.data() + static_cast<size_t>(t) * kin, kin, KP, R, t,
-                     blk.data());
+            pack_row(M.data() + static_cast<size_t>(t) * kin, L, t, blk.data());
         for (int trial = 0; trial < 50; trial++) {
             std::vector<uint32_t> x(kin);
             for (auto& v : x)
@@ -156,6 +157,78 @@ static void test_matrix(std::mt19937_64& g)
     std::printf("matrix dot2 path ok\n");
 }
 
+static void test_matrix_mfma(std::mt19937_64& g)
+{
+    for (int kin : {1, 3, 16, 17, 33, 64}) {
+        for (int R : {kin, 48}) {
+            int KP = 2;
+            while (KP < (kin + 1) / 2)
+                KP *= 2;
+            const MatLayout L{R, kin, KP};
+            if (!L.KS())
+                continue;  // small blocks stay on the dot2 kernel
+            std::vector<uint32_t> M(static_cast<size_t>(R) * kin);
+            for (auto& v : M) {
+                const int mode = static_cast<int>(g() % 8);
+                // force the residues that need row scaling or sit at the
+                // ends of the byte split
+                v = mode == 0   ? 32640u
+                    : mode == 1 ? 32767u + static_cast<uint32_t>(g() % 4)
+                    : mode == 2 ? 65536u - static_cast<uint32_t>(g() % 300)
+                                : static_cast<uint32_t>(g() % 65537);
+            }
+            std::vector<int32_t> blk(L.words());
+            for (int t = 0; t < R; t++)
+                pack_row(M.data() + static_cast<size_t>(t) * kin, L, t, blk.data());
+            for (size_t d = 0; d < L.mf_words(); d++)
+                blk[L.mf() + d] = pack_mf_dword(L, blk.data(), d);
+            const int KS = L.KS(), KH = 16 * KS;
+            auto opb = [&](int rb, int ks, int ty, int lane, int j) {
+                const size_t dw = L.mf() +
+                                  ((static_cast<size_t>(rb) * KS + ks) * 3 + ty) * 128 +
+                                  static_cast<size_t>(lane) * 2 + j / 4;
+                return static_cast<int>(static_cast<int8_t>(
+                    static_cast<uint32_t>(blk[dw]) >> (8 * (j % 4))));
+            };
+            for (int trial = 0; trial < 30; trial++) {
+                std::vector<uint32_t> x(kin);
+                for (auto& v : x)
+                    v = trial == 0 ? 0u : trial == 1 ? 65535u : static_cast<uint32_t>(g() % 65536);
+                for (int t = 0; t < R; t++) {
+                    const int rb = t / 16;
+                    // device: acc1 starts at kmf[t]; rows past kin hold a
+                    // clamped row (their operand bytes are 0)
+                    long long D[3] = {0, blk[L.kmf() + t], 0};
+                    for (int K = 0; K < 2 * KH; K++) {
+                        const int ks = K / 32, gg = (K % 32) / 8, j = K % 8;
+                        const int lane = 16 * gg + t % 16;
+                        const int i = K < KH ? K : K - KH;
+                        const uint32_t xi = x[i < kin ? i : kin - 1];
+                        const int byte = K < KH ? static_cast<int>(xi >> 8) - 128
+                                                : static_cast<int>(xi & 255) - 128;
+                        for (int ty = 0; ty < 3; ty++)
+                            D[ty] += static_cast<long long>(opb(rb, ks, ty, lane, j)) * byte;
+                    }
+                    for (long long d : D)
+                        CHECK(d >= -2147483648LL && d <= 2147483647LL, "mfma acc overflow");
+                    const long long v = D[2] * 256 + D[1] - D[0];
+                    CHECK(v >= -2147483648LL && v <= 2147483647LL, "mfma epilogue overflow");
+                    int32_t y = fold(fold(static_cast<int32_t>(v)));
+                    const int32_t rs = blk[L.rscale() + t];
+                    if (rs != 1)
+                        y = fold(fold(static_cast<int32_t>(static_cast<long long>(y) * rs)));
+                    long long ref = 0;
+                    for (int i = 0; i < kin; i++)
+                        ref = (ref + static_cast<long long>(M[static_cast<size_t>(t) * kin + i]) * x[i]) % 65537;
+                    CHECK(y >= -1 && y <= 65536, "mfma T range");
+                    CHECK(canon64(y) == static_cast<uint32_t>(ref), "mfma kin=%d R=%d t=%d", kin, R, t);
+                }
+            }
+        }
+    }
+    std::printf("matrix mfma path ok\n");
+}
+
 int main()
 {
     std::mt19937_64 g(12345);
@@ -174,6 +247,7 @@ int main()
     test_dft<32, -32767, 98303>(g);
     test_dft<64, -32767, 98303>(g);
     test_matrix(g);
+    test_matrix_mfma(g);
     if (fails) {
         std::printf("%d failures\n", fails);
         return 1;

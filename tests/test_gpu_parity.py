@@ -280,13 +280,15 @@ def test_empty_and_tiny_blocks(hip_lib):
         assert (outs == o_out).all() and (cnt == o_cnt).all()
 
 
-def test_dense_oor_tile_uses_bucket_scan():
+@pytest.mark.parametrize("k,m", [(16, 48), (32, 32)])
+def test_dense_oor_tile_uses_bucket_scan(k, m):
     """More than kRouteCap (15) marks of received rows inside one 1024-column
     tile: the decode falls back from the context's route table to scanning
-    the OOR buckets; output still bit-exact."""
+    the OOR buckets; output still bit-exact (k=16: dot2 kernel, k=32: the
+    matrix-core kernel)."""
     torch = _torch()
     import quadiron_amd as qa
-    k, m, S, P = 16, 48, 1, 2048
+    S, P = 1, 2048
     rng = np.random.default_rng(99)
     data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
     _craft(k, m, 0, data[0], rng, 200, rows=range(k), col_range=(512, 1024))
