@@ -11,6 +11,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <istream>
+#include <memory>
 #include <ostream>
 #include <utility>
 #include <vector>
@@ -121,6 +122,9 @@ class RsFnt {
                           std::vector<int>& ids) const;
 
     qi_plan* plan_ = nullptr;
+    // pinned two-slot pipeline of the stream API, kept across calls
+    struct StreamPipe;
+    std::unique_ptr<StreamPipe> pipe_;
 };
 
 // RS-NF4 (src/fec_rs_nf4.h:46-334, src/gf_nf4.h).  A word of word_size bytes

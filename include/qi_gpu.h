@@ -136,6 +136,22 @@ int qi_fec_decode_blocks(qi_fec* f, uint8_t** data, uint8_t** parities,
                          uint32_t oor_cap, const int* missing,
                          const int* wanted, size_t block_bytes);
 
+/* Stream API (encode_streams_vertical / decode_streams_vertical,
+ * src/fec_base.h:463-542, 898-1048) over caller memory: each fragment is a
+ * stream of `bytes` bytes.  The streams go through the two-slot pinned
+ * pipeline of qi::fec::RsFnt (chunks of whole packets, host reads/writes
+ * overlapping the transfers and kernels).  Encode: all outputs required;
+ * 0 or -1.  Decode: data[i] / parities[i] NULL = missing (data may be NULL
+ * as a whole for non-systematic codes), out_data[i] NULL = not wanted;
+ * 1 decoded, 0 fewer than k fragments, -1 error. */
+int qi_fec_encode_streams(qi_fec* f, const uint8_t** data, size_t bytes,
+                          uint8_t** outputs, uint32_t* oor, uint32_t* oor_count,
+                          uint32_t oor_cap);
+int qi_fec_decode_streams(qi_fec* f, const uint8_t** data,
+                          const uint8_t** parities, size_t bytes,
+                          const uint32_t* oor, const uint32_t* oor_count,
+                          uint32_t oor_cap, uint8_t** out_data);
+
 /* ---- RS-NF4 block API (C view of qi::fec::RsNf4; RsNf4<T>,
  * src/fec_rs_nf4.h:46-334).  word_size 2, 4 or 8 (NULL otherwise): every
  * word packs word_size/2 GF(65537) components, each coded like an RS-FNT

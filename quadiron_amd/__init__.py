@@ -60,6 +60,9 @@ def _declare(lib):
         "qi_fec_n_outputs": (I, [V]),
         "qi_fec_encode_blocks": (I, [V, c_u8pp, c_u8pp, SZ, V, V, U32]),
         "qi_fec_decode_blocks": (I, [V, c_u8pp, c_u8pp, V, V, U32, V, V, SZ]),
+        "qi_fec_encode_streams": (I, [V, c_u8pp, SZ, c_u8pp, V, V, U32]),
+        "qi_fec_decode_streams": (I, [V, c_u8pp, c_u8pp, SZ, V, V, U32,
+                                      c_u8pp]),
         "qi_nf4_new": (V, [I, I, I]),
         "qi_nf4_delete": (None, [V]),
         "qi_nf4_n_outputs": (I, [V]),

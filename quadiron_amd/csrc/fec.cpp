@@ -9,10 +9,12 @@
 #include <algorithm>
 #include <arpa/inet.h>
 #include <chrono>
+#include <memory>
 #include <cstring>
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 #include "../../include/qi_fec.hpp"
 #include "../../include/qi_gpu.h"
@@ -147,6 +149,7 @@ RsFnt::RsFnt(FecType t, unsigned ws, unsigned k, unsigned m, size_t pkt)
 
 RsFnt::~RsFnt()
 {
+    pipe_.reset();
     qi_plan_destroy(plan_);
 }
 
@@ -388,7 +391,7 @@ namespace {
 
 size_t chunk_bytes(size_t buf_size)
 {
-    const size_t target = 8u << 20;
+    const size_t target = 4u << 20;
     return buf_size * std::max<size_t>(1, target / buf_size);
 }
 
@@ -401,50 +404,206 @@ size_t read_full(std::istream* is, uint8_t* p, size_t len)
 
 }  // namespace
 
+namespace {
+
+// One stage of the pipelined stream API: pinned host staging, device
+// buffers and a HIP stream.  Chunk i runs in slot i % 2, so reading chunk i
+// from the input streams and writing chunk i-2 to the output streams overlap
+// the transfers and kernels of chunk i-1.
+struct StreamSlot {
+    hipStream_t st = nullptr;
+    uint8_t* host = nullptr;
+    size_t host_bytes = 0;
+    DevBuf in, out, small, ctx;
+    size_t got = 0, offset = 0;
+    uint32_t cap = 0;
+    bool busy = false;
+    StreamSlot()
+    {
+        check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    }
+    ~StreamSlot()
+    {
+        (void)hipStreamSynchronize(st);
+        if (host)
+            (void)hipHostFree(host);
+        in.release();
+        out.release();
+        small.release();
+        ctx.release();
+        (void)hipStreamDestroy(st);
+    }
+    StreamSlot(const StreamSlot&) = delete;
+    StreamSlot& operator=(const StreamSlot&) = delete;
+    uint8_t* pinned(size_t n)
+    {
+        if (n > host_bytes) {
+            if (host)
+                (void)hipHostFree(host);
+            host = nullptr;
+            host_bytes = 0;
+            check(hipHostMalloc(reinterpret_cast<void**>(&host), n,
+                                hipHostMallocDefault),
+                  "hipHostMalloc");
+            host_bytes = n;
+        }
+        return host;
+    }
+    void dev(DevBuf& b, size_t n)
+    {
+        if (!b.reserve(n))
+            throw std::runtime_error("RsFnt: device allocation failed");
+    }
+};
+
+size_t round64(size_t n)
+{
+    return (n + 63) / 64 * 64;
+}
+
+// fn(i) for i < n on up to 16 threads: the fragments are independent
+// streams (shard files, sockets), so they are read and written in parallel
+template <typename F>
+void parallel_for(size_t n, F fn)
+{
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = std::min<size_t>({n, hw, 16});
+    if (nt <= 1) {
+        for (size_t i = 0; i < n; i++)
+            fn(i);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < nt; t++)
+        pool.emplace_back([&, t] {
+            for (size_t i = t; i < n; i += nt)
+                fn(i);
+        });
+    for (auto& th : pool)
+        th.join();
+}
+
+// read `k` streams into rows `pitch` bytes apart: bytes read by every
+// stream (short = end of stream), the tail of each row zeroed
+size_t read_rows(const std::vector<std::istream*>& src, uint8_t* rows,
+                 size_t pitch, bool& cont)
+{
+    std::vector<size_t> r(src.size());
+    parallel_for(src.size(),
+                 [&](size_t i) { r[i] = read_full(src[i], rows + i * pitch, pitch); });
+    size_t got = pitch;
+    for (size_t i = 0; i < src.size(); i++) {
+        if (r[i] < pitch) {
+            got = std::min(got, r[i]);
+            cont = false;
+        }
+    }
+    for (size_t i = 0; i < src.size(); i++)
+        std::memset(rows + i * pitch + got, 0, pitch - got);
+    return got;
+}
+
+}  // namespace
+
+struct RsFnt::StreamPipe {
+    StreamSlot slot[2];
+};
+
 void RsFnt::encode_streams_vertical(
     const std::vector<std::istream*>& input_data_bufs,
     std::vector<std::ostream*>& output_parities_bufs,
     std::vector<Properties>& output_parities_props)
 {
     // src/fec_base.h:463-542: packets of buf_size bytes, zero padded tail,
-    // `read_bytes` of every output written for the last packet
+    // `read_bytes` of every output written for the last packet.  Here whole
+    // chunks of packets go through a two-slot pinned pipeline.
     for (auto& p : output_parities_props)
         p.clear();
     reset_stats_enc();
-    const size_t CH = chunk_bytes(buf_size);
-    std::vector<std::vector<uint8_t>> in(n_data, std::vector<uint8_t>(CH + 2));
-    std::vector<std::vector<uint8_t>> out(n_outputs, std::vector<uint8_t>(CH + 2));
-    size_t offset = 0;
-    bool cont = true;
-    while (cont) {
-        size_t got = CH;
-        for (unsigned i = 0; i < n_data; i++) {
-            const size_t r = read_full(input_data_bufs[i], in[i].data(), CH);
-            if (r < CH) {
-                got = r;
-                cont = false;
+    const size_t CH = chunk_bytes(buf_size);  // a multiple of 128 bytes
+    const size_t P = CH / 2, k = n_data, no = n_outputs;
+    const uint32_t cap = static_cast<uint32_t>(64 + P / 512);
+    // pinned: k input rows, no output rows, OOR counts, OOR entries
+    const size_t in_b = k * CH, out_b = no * CH, cnt_b = round64(no * 4);
+    const size_t ent_b = no * cap * 4;
+    if (!pipe_)
+        pipe_.reset(new StreamPipe);
+    StreamSlot* slot = pipe_->slot;
+    Timer tm;
+    auto finish = [&](StreamSlot& sl) {
+        check(hipStreamSynchronize(sl.st), "sync");
+        sl.busy = false;
+        uint8_t* hout = sl.host + in_b;
+        const uint32_t* cnt = reinterpret_cast<const uint32_t*>(hout + out_b);
+        const uint32_t* ent = reinterpret_cast<const uint32_t*>(hout + out_b + cnt_b);
+        const size_t words = (sl.got + 1) / 2;
+        const uint32_t mx = *std::max_element(cnt, cnt + no);
+        if (mx > cap) {
+            // adversarial data: redo this chunk synchronously, exact capacity
+            std::vector<const uint8_t*> dp(k);
+            std::vector<uint8_t*> op(no);
+            for (size_t i = 0; i < k; i++)
+                dp[i] = sl.host + i * CH;
+            for (size_t i = 0; i < no; i++)
+                op[i] = hout + i * CH;
+            encode_columns(dp.data(), op.data(), words, output_parities_props,
+                           sl.offset);
+        } else {
+            for (size_t i = 0; i < no; i++) {
+                std::vector<uint32_t> b(ent + i * cap, ent + i * cap + cnt[i]);
+                std::sort(b.begin(), b.end());
+                for (uint32_t e : b)
+                    output_parities_props[i].add(sl.offset + e, OOR_MARK);
             }
         }
+        parallel_for(no, [&](size_t i) {
+            output_parities_bufs[i]->write(reinterpret_cast<const char*>(hout + i * CH),
+                                           static_cast<std::streamsize>(sl.got));
+        });
+    };
+    size_t offset = 0;
+    unsigned it = 0;
+    bool cont = true;
+    while (cont) {
+        StreamSlot& sl = slot[it & 1];
+        if (sl.busy)
+            finish(sl);
+        uint8_t* h = sl.pinned(in_b + out_b + cnt_b + ent_b);
+        const size_t got = read_rows(input_data_bufs, h, CH, cont);
         if (got == 0)
             break;
-        for (unsigned i = 0; i < n_data; i++)
-            std::fill(in[i].begin() + got, in[i].end(), 0);
-        std::vector<const uint8_t*> dp(n_data);
-        std::vector<uint8_t*> op(n_outputs);
-        for (unsigned i = 0; i < n_data; i++)
-            dp[i] = in[i].data();
-        for (unsigned i = 0; i < n_outputs; i++)
-            op[i] = out[i].data();
-        Timer tm;
-        encode_columns(dp.data(), op.data(), (got + 1) / 2, output_parities_props,
-                       offset);
-        total_enc_usec += tm.usec();
-        n_encode_ops++;
-        for (unsigned i = 0; i < n_outputs; i++)
-            output_parities_bufs[i]->write(reinterpret_cast<char*>(out[i].data()),
-                                           static_cast<std::streamsize>(got));
+        const size_t words = (got + 1) / 2;
+        sl.dev(sl.in, in_b);
+        sl.dev(sl.out, out_b);
+        sl.dev(sl.small, cnt_b + ent_b);
+        uint32_t* dcnt = static_cast<uint32_t*>(sl.small.p);
+        uint32_t* dent = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(sl.small.p) + cnt_b);
+        check(hipMemcpyAsync(sl.in.p, h, k * CH, hipMemcpyHostToDevice, sl.st), "H2D");
+        check_rc(qi_gpu_oor_clear(dcnt, no, sl.st), "oor_clear");
+        check_rc(qi_gpu_encode(plan_, static_cast<uint16_t*>(sl.in.p), 0,
+                               static_cast<long long>(P),
+                               static_cast<uint16_t*>(sl.out.p), 0,
+                               static_cast<long long>(P), static_cast<long long>(words),
+                               1, dcnt, dent, static_cast<int>(cap), sl.st),
+                 "qi_gpu_encode");
+        check(hipMemcpyAsync(h + in_b, sl.out.p, out_b, hipMemcpyDeviceToHost, sl.st),
+              "D2H");
+        check(hipMemcpyAsync(h + in_b + out_b, sl.small.p, cnt_b + ent_b,
+                             hipMemcpyDeviceToHost, sl.st),
+              "D2H");
+        sl.got = got;
+        sl.offset = offset;
+        sl.busy = true;
         offset += got / 2;
+        n_encode_ops++;
+        it++;
     }
+    // drain in chunk order: the older pending chunk sits in slot it % 2
+    if (slot[it & 1].busy)
+        finish(slot[it & 1]);
+    if (slot[(it + 1) & 1].busy)
+        finish(slot[(it + 1) & 1]);
+    total_enc_usec += tm.usec();
 }
 
 bool RsFnt::decode_streams_vertical(
@@ -453,7 +612,8 @@ bool RsFnt::decode_streams_vertical(
     std::vector<Properties>& input_parities_props,
     std::vector<std::ostream*>& output_data_bufs)
 {
-    // src/fec_base.h:898-1048
+    // src/fec_base.h:898-1048, through the same two-slot pipeline: the k
+    // received rows of a chunk are staged back to back (packed decode)
     const bool sys = type == FecType::SYSTEMATIC;
     std::vector<int> present(code_len, 0);
     if (sys)
@@ -474,52 +634,114 @@ bool RsFnt::decode_streams_vertical(
     for (auto& p : input_parities_props)
         p.sort();
     reset_stats_dec();
-    std::vector<std::istream*> src(n_data);
-    std::vector<const Properties*> props(n_data, nullptr);
-    for (unsigned i = 0; i < n_data; i++) {
+    const size_t k = n_data;
+    std::vector<std::istream*> src(k);
+    // OOR marks of each received row (ascending), consumed chunk by chunk
+    std::vector<std::vector<size_t>> marks(k);
+    for (size_t i = 0; i < k; i++) {
         const int id = ids[i];
         if (sys && id < static_cast<int>(n_data)) {
             src[i] = input_data_bufs[id];
         } else {
-            const int slot = sys ? id - static_cast<int>(n_data) : id;
-            src[i] = input_parities_bufs[slot];
-            props[i] = &input_parities_props[slot];
+            const int s_ = sys ? id - static_cast<int>(n_data) : id;
+            src[i] = input_parities_bufs[s_];
+            for (auto const& it : input_parities_props[s_].get_map())
+                marks[i].push_back(it.first);
         }
     }
+    std::vector<size_t> mpos(k, 0);
     const size_t CH = chunk_bytes(buf_size);
-    std::vector<std::vector<uint8_t>> in(n_data, std::vector<uint8_t>(CH + 2));
-    std::vector<std::vector<uint8_t>> out(n_data, std::vector<uint8_t>(CH + 2));
+    const size_t P = CH / 2;
+    const size_t io_b = k * CH, ids_b = round64(k * 2), cnt_b = round64(k * 4);
+    const size_t ctx_b = qi_gpu_decode_ctx_bytes(plan_, 1, static_cast<long long>(P));
+    if (!pipe_)
+        pipe_.reset(new StreamPipe);
+    StreamSlot* slot = pipe_->slot;
+    Timer tm;
+    auto finish = [&](StreamSlot& sl) {
+        check(hipStreamSynchronize(sl.st), "sync");
+        sl.busy = false;
+        if (qi_gpu_take_error(plan_))
+            throw std::runtime_error("RsFnt: too many OOR marks in one tile");
+        const uint8_t* hout = sl.host + io_b;
+        parallel_for(k, [&](size_t i) {
+            if (output_data_bufs[i])
+                output_data_bufs[i]->write(reinterpret_cast<const char*>(hout + i * CH),
+                                           static_cast<std::streamsize>(sl.got));
+        });
+    };
     size_t offset = 0;
+    unsigned it = 0;
     bool cont = true;
     while (cont) {
-        size_t got = CH;
-        for (unsigned i = 0; i < n_data; i++) {
-            const size_t r = read_full(src[i], in[i].data(), CH);
-            if (r < CH) {
-                got = r;
-                cont = false;
-            }
+        StreamSlot& sl = slot[it & 1];
+        if (sl.busy)
+            finish(sl);
+        // the chunk's marks per received row (positions relative to it)
+        const size_t words_max = P;
+        std::vector<std::vector<uint32_t>> cm(k);
+        uint32_t cap = 1;
+        for (size_t i = 0; i < k; i++) {
+            while (mpos[i] < marks[i].size() && marks[i][mpos[i]] < offset)
+                mpos[i]++;
+            size_t e = mpos[i];
+            while (e < marks[i].size() && marks[i][e] < offset + words_max)
+                cm[i].push_back(static_cast<uint32_t>(marks[i][e++] - offset));
+            cap = std::max<uint32_t>(cap, static_cast<uint32_t>(cm[i].size()));
         }
+        const size_t ent_b = round64(static_cast<size_t>(k) * cap * 4);
+        const size_t small_b = ids_b + cnt_b + ent_b;
+        uint8_t* h = sl.pinned(2 * io_b + small_b);
+        const size_t got = read_rows(src, h, CH, cont);
         if (got == 0)
             break;
-        for (unsigned i = 0; i < n_data; i++)
-            std::fill(in[i].begin() + got, in[i].end(), 0);
-        std::vector<const uint8_t*> rp(n_data);
-        std::vector<uint8_t*> op(n_data);
-        for (unsigned i = 0; i < n_data; i++) {
-            rp[i] = in[i].data();
-            op[i] = output_data_bufs[i] ? out[i].data() : nullptr;
+        const size_t words = (got + 1) / 2;
+        uint8_t* hs = h + 2 * io_b;
+        uint16_t* hids = reinterpret_cast<uint16_t*>(hs);
+        uint32_t* hcnt = reinterpret_cast<uint32_t*>(hs + ids_b);
+        uint32_t* hent = reinterpret_cast<uint32_t*>(hs + ids_b + cnt_b);
+        for (size_t i = 0; i < k; i++) {
+            hids[i] = static_cast<uint16_t>(ids[i]);
+            hcnt[i] = static_cast<uint32_t>(cm[i].size());
+            std::copy(cm[i].begin(), cm[i].end(), hent + i * cap);
         }
-        Timer tm;
-        decode_columns(ids, rp, props, op.data(), (got + 1) / 2, offset);
-        total_dec_usec += tm.usec();
-        n_decode_ops++;
-        for (unsigned i = 0; i < n_data; i++)
-            if (output_data_bufs[i])
-                output_data_bufs[i]->write(reinterpret_cast<char*>(out[i].data()),
-                                           static_cast<std::streamsize>(got));
+        sl.dev(sl.in, io_b);
+        sl.dev(sl.out, io_b);
+        sl.dev(sl.small, small_b);
+        sl.dev(sl.ctx, ctx_b);
+        uint8_t* ds = static_cast<uint8_t*>(sl.small.p);
+        const uint16_t* dids = reinterpret_cast<const uint16_t*>(ds);
+        const uint32_t* dcnt = reinterpret_cast<const uint32_t*>(ds + ids_b);
+        const uint32_t* dent = reinterpret_cast<const uint32_t*>(ds + ids_b + cnt_b);
+        check(hipMemcpyAsync(sl.in.p, h, io_b, hipMemcpyHostToDevice, sl.st), "H2D");
+        check(hipMemcpyAsync(sl.small.p, hs, small_b, hipMemcpyHostToDevice, sl.st),
+              "H2D");
+        check_rc(qi_gpu_decode_ctx_packed(plan_, dids, hids, 1, dcnt, dent,
+                                          static_cast<int>(cap),
+                                          static_cast<long long>(words), sl.ctx.p,
+                                          sl.st),
+                 "decode context");
+        check_rc(qi_gpu_decode_packed(plan_, sl.ctx.p, static_cast<uint16_t*>(sl.in.p),
+                                      0, static_cast<long long>(P), dcnt, dent,
+                                      static_cast<int>(cap),
+                                      static_cast<uint16_t*>(sl.out.p), 0,
+                                      static_cast<long long>(P),
+                                      static_cast<long long>(words), 1, sl.st),
+                 "decode");
+        check(hipMemcpyAsync(h + io_b, sl.out.p, io_b, hipMemcpyDeviceToHost, sl.st),
+              "D2H");
+        sl.got = got;
+        sl.offset = offset;
+        sl.busy = true;
         offset += got / 2;
+        n_decode_ops++;
+        it++;
     }
+    if (slot[it & 1].busy)
+        finish(slot[it & 1]);
+    if (slot[(it + 1) & 1].busy)
+        finish(slot[(it + 1) & 1]);
+    total_dec_usec += tm.usec();
     return true;
 }
 
@@ -720,6 +942,112 @@ int qi_fec_decode_blocks(qi_fec* h, uint8_t** data, uint8_t** parities,
             want[i] = wanted[i] != 0;
         return f.decode_blocks_vertical(dv, pv, props, miss, want, block_bytes) ? 1
                                                                                 : 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
+}  // extern "C"
+
+namespace {
+
+// std::streambuf over caller memory (no copies of its own) for the C view
+// of the stream API
+struct MemIn : std::streambuf {
+    MemIn(const uint8_t* p, size_t n)
+    {
+        char* b = reinterpret_cast<char*>(const_cast<uint8_t*>(p));
+        setg(b, b, b + n);
+    }
+};
+struct MemOut : std::streambuf {
+    MemOut(uint8_t* p, size_t n)
+    {
+        char* b = reinterpret_cast<char*>(p);
+        setp(b, b + n);
+    }
+};
+
+struct MemStreams {
+    std::vector<std::unique_ptr<std::streambuf>> bufs;
+    std::vector<std::unique_ptr<std::iostream>> streams;
+    std::iostream* in(const uint8_t* p, size_t n)
+    {
+        if (!p)
+            return nullptr;
+        bufs.emplace_back(new MemIn(p, n));
+        streams.emplace_back(new std::iostream(bufs.back().get()));
+        return streams.back().get();
+    }
+    std::iostream* out(uint8_t* p, size_t n)
+    {
+        if (!p)
+            return nullptr;
+        bufs.emplace_back(new MemOut(p, n));
+        streams.emplace_back(new std::iostream(bufs.back().get()));
+        return streams.back().get();
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int qi_fec_encode_streams(qi_fec* h, const uint8_t** data, size_t bytes,
+                          uint8_t** outputs, uint32_t* oor, uint32_t* oor_count,
+                          uint32_t cap)
+{
+    try {
+        qi::fec::RsFnt& f = *h->f;
+        MemStreams ms;
+        std::vector<std::istream*> in(f.n_data);
+        std::vector<std::ostream*> out(f.n_outputs);
+        for (unsigned i = 0; i < f.n_data; i++)
+            if (!(in[i] = ms.in(data[i], bytes)))
+                return -1;
+        for (unsigned i = 0; i < f.n_outputs; i++)
+            if (!(out[i] = ms.out(outputs[i], bytes)))
+                return -1;
+        std::vector<qi::Properties> props(f.n_outputs);
+        f.encode_streams_vertical(in, out, props);
+        for (unsigned i = 0; i < f.n_outputs; i++) {
+            uint32_t c = 0;
+            for (auto const& it : props[i].get_map()) {
+                if (c < cap)
+                    oor[static_cast<size_t>(i) * cap + c] =
+                        static_cast<uint32_t>(it.first);
+                c++;
+            }
+            oor_count[i] = c;
+        }
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
+int qi_fec_decode_streams(qi_fec* h, const uint8_t** data,
+                          const uint8_t** parities, size_t bytes,
+                          const uint32_t* oor, const uint32_t* oor_count,
+                          uint32_t cap, uint8_t** out_data)
+{
+    try {
+        qi::fec::RsFnt& f = *h->f;
+        MemStreams ms;
+        std::vector<std::istream*> din(f.n_data), pin(f.n_outputs);
+        std::vector<std::ostream*> dout(f.n_data);
+        for (unsigned i = 0; i < f.n_data; i++) {
+            din[i] = ms.in(data ? data[i] : nullptr, bytes);
+            dout[i] = ms.out(out_data[i], bytes);
+        }
+        std::vector<qi::Properties> props(f.n_outputs);
+        for (unsigned i = 0; i < f.n_outputs; i++) {
+            pin[i] = ms.in(parities[i], bytes);
+            const uint32_t c = oor_count[i] < cap ? oor_count[i] : cap;
+            for (uint32_t e = 0; e < c; e++)
+                props[i].add(oor[static_cast<size_t>(i) * cap + e], qi::OOR_MARK);
+        }
+        return f.decode_streams_vertical(din, pin, props, dout) ? 1 : 0;
     } catch (...) {
         return -1;
     }

@@ -88,6 +88,42 @@ __global__ __launch_bounds__(BT) void enc(const uint16_t* in, uint16_t* out, int
 }
 
 
+
+// encode shape with half-wave pass split: a block covers 256 columns (each
+// column read by 2 lanes); lanes 0-31 of a wave store row 4u+v, lanes 32-63
+// row 4u+v+1 (v even), 4 B per lane: every store instruction writes 128 B of
+// two rows whose 64 KiB address bit differs
+template <int ORD, int AUXS>
+__global__ __launch_bounds__(256) void enc_split(const uint16_t* in, uint16_t* out, int S,
+                                                 int tiles)
+{
+    const int b = blockIdx.x;
+    int s, tile;
+    if constexpr (ORD == 0) {
+        s = b / tiles;
+        tile = b % tiles;
+    } else {
+        const int xcd = b & 7, j = b >> 3;
+        s = (j / tiles) * 8 + xcd;
+        tile = j % tiles;
+    }
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, h = l >> 5;
+    const uint32_t voff = (tile * 128 + w * 32 + (l & 31)) * 4;
+    auto ri = rsrc(in + (long)s * 16 * P, 16 * P * 2);
+    auto ro = rsrc(out + (long)s * 64 * P, 64 * P * 2);
+    uint32_t x[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+        x[t] = __builtin_amdgcn_raw_buffer_load_b32(ri, voff, t * P * 2, 0);
+    const uint32_t vo = voff + h * P * 2;
+#pragma unroll
+    for (int pp = 0; pp < 2; pp++)
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            __builtin_amdgcn_raw_buffer_store_b32(x[u] ^ (u * 0x9E3779B9u), ro, vo,
+                                                  (4 * u + 2 * pp) * P * 2, AUXS);
+}
+
 // decode shape: 16 of a stripe's 64 rows in (8 B per lane), 16 rows out
 template <int ORD, int AUXL, int AUXS>
 __global__ __launch_bounds__(256) void dec(const uint16_t* in, uint16_t* out, int S, int tiles)
@@ -158,8 +194,17 @@ int main(int argc, char** argv)
     for (int rep = 0; rep < 3; rep++) {
     printf("--- rep %d\n", rep);
     RUN(256, 0, 1, 0, 2)
+    RUN(256, 3, 1, 0, 18)
     RUN(256, 3, 2, 0, 18)
-    RUN(256, 3, 2, 0, 26)
+#define SPLIT(ORD, SA)                                                            \
+    {                                                                             \
+        const int tiles = P / 128;                                                \
+        float ms = timeit([&] { enc_split<ORD, SA><<<tiles * S, 256>>>(a, b, S, tiles); }, reps); \
+        printf("enc split ord%d S%2d        %7.3f ms %7.1f GB/s\n", ORD, SA, ms, eb / ms / 1e6); \
+    }
+    SPLIT(0, 2)
+    SPLIT(3, 18)
+    SPLIT(3, 2)
 #define DEC(ORD, L, SA)                                                              \
     {                                                                                \
         const int tiles = P / 1024;                                                  \
