@@ -237,11 +237,9 @@ def main():
     metric = ("device-resident encode+decode GB/s per GPU, RS-FNT k=16 n=64 "
               "pkt=64KiB" if headline else
               f"device-resident encode+decode GB/s per GPU, {name}")
-    # the matrix path runs on the matrix cores above 16 x 16 products per
-    # column (matrix_pack.h MatLayout::KS), on the dot2 kernel otherwise
-    enc_rows = m if sys_ else plan.n_outputs
-    mat_kernel = ("matrix_mfma_kernel<*>" if k <= 64 and enc_rows * k > 256
-                  else "matrix_kernel<*>")
+    # the matrix path runs on the matrix cores for k <= 64
+    # (matrix_pack.h MatLayout::KS), on the dot2 kernel otherwise
+    mat_kernel = "matrix_mfma_kernel<*>" if k <= 64 else "matrix_kernel<*>"
     enc_kernel = (f"encode_fnt_kernel<{K},*>" if not sys_ and K <= 64
                   else mat_kernel)
     out = {

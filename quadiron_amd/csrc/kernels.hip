@@ -1013,15 +1013,40 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                     }
                 }
             }
-            if (trow) {
-                qi_v4u o0, o1;
+            qi_v4u o0, o1;
 #pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    o0[c] = pack_lo(static_cast<uint32_t>(y[2 * c]),
-                                    static_cast<uint32_t>(y[2 * c + 1]));
-                    o1[c] = pack_lo(static_cast<uint32_t>(y[8 + 2 * c]),
-                                    static_cast<uint32_t>(y[8 + 2 * c + 1]));
+            for (int c = 0; c < 4; c++) {
+                o0[c] = pack_lo(static_cast<uint32_t>(y[2 * c]),
+                                static_cast<uint32_t>(y[2 * c + 1]));
+                o1[c] = pack_lo(static_cast<uint32_t>(y[8 + 2 * c]),
+                                static_cast<uint32_t>(y[8 + 2 * c + 1]));
+            }
+            if (RB == 1) {
+                // one block of output rows: this super tile's input bytes
+                // are dead once its MFMAs are done, so the 16 x 64 output
+                // tile is transposed through them (row t at image rows 2t,
+                // 2t+1, bytes 64 ST..) and stored as 8 whole 128-byte lines
+                // per instruction -- which can stream (nt|sc1)
+                uint8_t* stg = img + 64 * ST;
+                *reinterpret_cast<qi_v4u*>(stg + (2 * tl + (g >> 1)) * RSB + 32 * (g & 1)) = o0;
+                *reinterpret_cast<qi_v4u*>(stg + (2 * tl + (g >> 1)) * RSB + 32 * (g & 1) + 16) = o1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int orow = 8 * h + (l >> 3), c = l & 7;
+                    const qi_v4u v = *reinterpret_cast<const qi_v4u*>(
+                        stg + (2 * orow + (c >> 2)) * RSB + 16 * (c & 3));
+                    if (orow < L.R) {
+                        const uint32_t vo =
+                            static_cast<uint32_t>(orow) * ors +
+                            static_cast<uint32_t>((col0 + 64 * ST + 8 * c) * 2);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo),
+                                                               0, kAuxSt);
+                    }
                 }
+            } else if (trow) {
                 const uint32_t vo = static_cast<uint32_t>(t) * ors +
                                     static_cast<uint32_t>(cb * 2);
                 __builtin_amdgcn_raw_buffer_store_b128(o0, go.r, static_cast<int>(vo),
