@@ -89,13 +89,6 @@ struct Region {
 #endif
 constexpr int kAuxLd = QI_AUX_LD;
 constexpr int kAuxSt = QI_AUX_ST;
-// the matrix-core kernel's stores cover a 128-byte line in two 16-byte
-// halves per lane group: default policy, so the L2 merges them into whole
-// lines (streaming nt|sc1 stores would reach HBM as partial lines)
-#ifndef QI_MFMA_AUX_ST
-#define QI_MFMA_AUX_ST 0
-#endif
-constexpr int kAuxStMf = QI_MFMA_AUX_ST;
 
 // XCD-aware block -> (stripe, tile) map.  Workgroups are dispatched
 // round-robin over the 8 XCDs (block b runs on XCD b % 8), so with the plain
@@ -781,6 +774,11 @@ struct MfmaTile {
     static constexpr size_t kImg = static_cast<size_t>(2 * kRows) * kPitch;
     // image + OOR scan scratch (s_i, s_col) + s_cnt
     static constexpr size_t kLds = kImg + 2 * 4 * kMaxTileOor + 16;
+    // per-wave output staging tile (16 rows x 128 bytes, padded), only
+    // allocated when the block has several 16-row output blocks
+    static constexpr int kStagePitch = 144;
+    static constexpr size_t kStage = 16 * kStagePitch;
+    static constexpr size_t kLdsStaged = kLds + 4 * kStage;
 };
 
 template <int KS, int COLS>
@@ -1021,40 +1019,48 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                 o1[c] = pack_lo(static_cast<uint32_t>(y[8 + 2 * c]),
                                 static_cast<uint32_t>(y[8 + 2 * c + 1]));
             }
+            // the 16 x 64 output tile is transposed through LDS and stored
+            // as 8 whole 128-byte lines per instruction, which can stream
+            // (nt|sc1).  One block of output rows: through this super
+            // tile's input bytes, dead once its MFMAs are done (row t at
+            // image rows 2t, 2t+1, bytes 64 ST..); several: through the
+            // wave's own staging tile behind the image (144-byte rows).
+            uint8_t* stg;
+            int pitch, half;
             if (RB == 1) {
-                // one block of output rows: this super tile's input bytes
-                // are dead once its MFMAs are done, so the 16 x 64 output
-                // tile is transposed through them (row t at image rows 2t,
-                // 2t+1, bytes 64 ST..) and stored as 8 whole 128-byte lines
-                // per instruction -- which can stream (nt|sc1)
-                uint8_t* stg = img + 64 * ST;
-                *reinterpret_cast<qi_v4u*>(stg + (2 * tl + (g >> 1)) * RSB + 32 * (g & 1)) = o0;
-                *reinterpret_cast<qi_v4u*>(stg + (2 * tl + (g >> 1)) * RSB + 32 * (g & 1) + 16) = o1;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int orow = 8 * h + (l >> 3), c = l & 7;
-                    const qi_v4u v = *reinterpret_cast<const qi_v4u*>(
-                        stg + (2 * orow + (c >> 2)) * RSB + 16 * (c & 3));
-                    if (orow < L.R) {
-                        const uint32_t vo =
-                            static_cast<uint32_t>(orow) * ors +
-                            static_cast<uint32_t>((col0 + 64 * ST + 8 * c) * 2);
-                        __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo),
-                                                               0, kAuxSt);
-                    }
-                }
-            } else if (trow) {
-                const uint32_t vo = static_cast<uint32_t>(t) * ors +
-                                    static_cast<uint32_t>(cb * 2);
-                __builtin_amdgcn_raw_buffer_store_b128(o0, go.r, static_cast<int>(vo),
-                                                       0, kAuxStMf);
-                __builtin_amdgcn_raw_buffer_store_b128(o1, go.r,
-                                                       static_cast<int>(vo + 16), 0,
-                                                       kAuxStMf);
+                stg = img + 64 * ST;
+                pitch = 2 * RSB;
+                half = RSB - 64;  // bytes 64..127 of a row sit one image row down
+            } else {
+                stg = qi_lds + G::kLds + wv * G::kStage;
+                pitch = G::kStagePitch;
+                half = 0;
             }
+            auto at = [&](int row, int byte) {
+                return stg + row * pitch + byte + (byte >= 64 ? half : 0);
+            };
+            *reinterpret_cast<qi_v4u*>(at(tl, 32 * g)) = o0;
+            *reinterpret_cast<qi_v4u*>(at(tl, 32 * g + 16)) = o1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int orow = 8 * h + (l >> 3), c = l & 7;
+                const qi_v4u v = *reinterpret_cast<const qi_v4u*>(at(orow, 16 * c));
+                const int ot = 16 * rb + orow;
+                if (ot < L.R) {
+                    const uint32_t vo =
+                        static_cast<uint32_t>(ot) * ors +
+                        static_cast<uint32_t>((col0 + 64 * ST + 8 * c) * 2);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo),
+                                                           0, kAuxSt);
+                }
+            }
+            // the staging tile is rewritten by the next (ST, rb): keep this
+            // iteration's reads ahead of those writes
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
         if (rb + 1 < RB) {
 #pragma unroll
@@ -1395,17 +1401,18 @@ static int mfma_launch(const MatLayout& L, const int32_t* mat, long long ms,
     const long long t = wfull / G::kCols;
     if (t <= 0 || t * S > 0x7fffffffLL)
         return -1;
+    const size_t lds = L.RB() > 1 ? G::kLdsStaged : G::kLds;
     static bool attr = false;  // dynamic LDS above 64 KiB needs opting in
-    if (G::kLds > 65536 && !attr) {
+    if (G::kLdsStaged > 65536 && !attr) {
         if (hipFuncSetAttribute(
                 reinterpret_cast<const void*>(&matrix_mfma_kernel<KS, COLS>),
                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                static_cast<int>(G::kLds)) != hipSuccess)
+                static_cast<int>(G::kLdsStaged)) != hipSuccess)
             return -2;
         attr = true;
     }
     hipLaunchKernelGGL((matrix_mfma_kernel<KS, COLS>), dim3(t * S), dim3(kBlock),
-                       G::kLds, st, L, mat, ms, ids, is, src, dst, ext, words,
+                       lds, st, L, mat, ms, ids, is, src, dst, ext, words,
                        static_cast<int>(t), io, slot_base, oo, route, rstride,
                        err);
     return hipGetLastError() == hipSuccess ? 0 : -2;
