@@ -56,9 +56,16 @@ QI_HD uint32_t canon(int64_t x)
     return static_cast<uint32_t>(r < 0 ? r + kQ : r);
 }
 
+// a * b mod q for a, b in [0, 65536]: with 2^16 = -1 and 2^32 = 1 the
+// product p0 + p1 2^16 + p2 2^32 reduces to p0 - p1 + p2 (no 64-bit modulo,
+// which is a long software sequence on the GPU)
 constexpr uint32_t mulmod_c(uint32_t a, uint32_t b)
 {
-    return static_cast<uint32_t>((static_cast<uint64_t>(a) * b) % 65537u);
+    const uint64_t p = static_cast<uint64_t>(a % 65537u) * (b % 65537u);
+    const int32_t v = static_cast<int32_t>(p & 0xffffu) -
+                      static_cast<int32_t>((p >> 16) & 0xffffu) +
+                      static_cast<int32_t>(p >> 32);  // [-65535, 65536]
+    return static_cast<uint32_t>(v < 0 ? v + 65537 : v);
 }
 
 constexpr uint32_t powmod_c(uint32_t a, uint32_t e)

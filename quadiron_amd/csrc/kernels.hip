@@ -1121,8 +1121,12 @@ __global__ __launch_bounds__(64) void decode_ctx_kernel(
 {
     __shared__ uint32_t xs[64];
     __shared__ uint32_t A[65];
-    __shared__ uint32_t Mt[64 * 64];
-    __shared__ uint32_t Qt[64 * 64];  // Q_i coefficients (systematic mode)
+    // k x k matrix (and the Q_i coefficients in systematic mode), sized by
+    // the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
+    // limited the kernel to 4 workgroups per CU
+    extern __shared__ uint32_t qi_ctx_lds[];
+    uint32_t* Mt = qi_ctx_lds;
+    uint32_t* Qt = qi_ctx_lds + k * k;
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
     int32_t* mat = ctx + s * ctx_stride;
@@ -1494,7 +1498,8 @@ int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
     if (k > 64 || S <= 0)
         return -3;
     Oor none{nullptr, nullptr, 0, 0};
-    hipLaunchKernelGGL(decode_ctx_kernel, dim3(S), dim3(64), 0, st, k, r, mode,
+    const size_t lds = static_cast<size_t>(k) * k * 4 * (mode ? 2 : 1);
+    hipLaunchKernelGGL(decode_ctx_kernel, dim3(S), dim3(64), lds, st, k, r, mode,
                        L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
                        slot_base, by_pos, words);
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -84,20 +84,20 @@ QI_HD void pack_row(const uint32_t* row, const MatLayout& L, int t,
                     int32_t* block)
 {
     const int kin = L.kin, KP = L.KP;
+    // s = 1 almost always (a row needs scaling with probability ~ 5 kin /
+    // 65537): test it without multiplications
+    bool ok = true;
+    for (int i = 0; i < kin && ok; i++)
+        ok = coef_ok(balanced(row[i]));
     uint32_t s = 1;
-    for (;; s++) {
+    for (; !ok;) {
+        s++;
         const int32_t si = balanced(powmod_c(s, 65535u));
         if (iabs32(si) > 32766)
             continue;
-        bool ok = true;
-        for (int i = 0; i < kin; i++) {
-            if (!coef_ok(balanced(mulmod_c(row[i], s)))) {
-                ok = false;
-                break;
-            }
-        }
-        if (ok)
-            break;
+        ok = true;
+        for (int i = 0; i < kin && ok; i++)
+            ok = coef_ok(balanced(mulmod_c(row[i], s)));
     }
     int32_t* packed = block + static_cast<size_t>(t) * KP;
     int32_t* plain = block + L.plain();
@@ -118,7 +118,7 @@ QI_HD void pack_row(const uint32_t* row, const MatLayout& L, int t,
     }
     const uint32_t sq = static_cast<uint32_t>(sum % 65537u);
     block[L.kcorr() + t] = static_cast<int32_t>(mulmod_c(sq, 32768u));
-    block[L.rscale() + t] = balanced(powmod_c(s, 65535u));
+    block[L.rscale() + t] = s == 1 ? 1 : balanced(powmod_c(s, 65535u));
     if (L.KS())
         block[L.kmf() + t] = static_cast<int32_t>(mulmod_c(sq, 32896u));
 }
