@@ -1114,7 +1114,11 @@ __device__ __forceinline__ uint32_t powm(uint32_t b, uint32_t e)
     return r;
 }
 
-__global__ __launch_bounds__(64) void decode_ctx_kernel(
+// NT threads: the Lagrange part runs on the first wave (lane = point); the
+// row packing and the MFMA operand tiles use every thread (NT = 256 for
+// k > 32, where they dominate and there are few stripes per launch)
+template <int NT>
+__global__ __launch_bounds__(NT) void decode_ctx_kernel(
     int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
     int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
     int by_pos, long long words)
@@ -1132,12 +1136,12 @@ __global__ __launch_bounds__(64) void decode_ctx_kernel(
     int32_t* mat = ctx + s * ctx_stride;
     int32_t* cids = mat + L.words();
     uint32_t* route = reinterpret_cast<uint32_t*>(cids + 2 * L.KP);
-    for (int i = k + tid; i < 2 * L.KP; i += 64)
+    for (int i = k + tid; i < 2 * L.KP; i += NT)
         cids[i] = 0;
     const long long ntiles = route_tiles(words);
 
     // route table: clear, then (after the barrier below) fill
-    for (long long t = tid; t < ntiles; t += 64)
+    for (long long t = tid; t < ntiles; t += NT)
         route[t * kRouteStride] = 0;
     if (tid < k) {
         const uint32_t id = ids[static_cast<long long>(s) * k + tid];
@@ -1166,16 +1170,18 @@ __global__ __launch_bounds__(64) void decode_ctx_kernel(
     }
     // A(x) = prod_i (x - x_i), lane d holding coefficient d (A is monic:
     // A[k] = 1 is set explicitly, so k = 64 needs no 65th lane)
-    uint32_t a = tid == 0 ? 1u : 0u;
-    for (int i = 0; i < k; i++) {
-        uint32_t prev = __shfl_up(a, 1);
+    if (tid < 64) {  // wave 0 (wave-uniform)
+        uint32_t a = tid == 0 ? 1u : 0u;
+        for (int i = 0; i < k; i++) {
+            uint32_t prev = __shfl_up(a, 1);
+            if (tid == 0)
+                prev = 0;
+            a = subm(prev, mulm(xs[i], a));
+        }
+        A[tid] = a;
         if (tid == 0)
-            prev = 0;
-        a = subm(prev, mulm(xs[i], a));
+            A[k] = 1;
     }
-    A[tid] = a;
-    if (tid == 0)
-        A[k] = 1;
     __syncthreads();
     if (tid < k) {
         // 1 / A'(x_i) = 1 / prod_{j != i} (x_i - x_j)
@@ -1207,14 +1213,18 @@ __global__ __launch_bounds__(64) void decode_ctx_kernel(
         }
     }
     __syncthreads();
-    for (int t = tid; t < L.R; t += 64)
-        pack_row(Mt + t * k, L, t, mat);
+    for (int t = tid; t < L.R; t += NT) {
+        const uint32_t sc = pack_row(Mt + t * k, L, t, mat);
+        if (sc != 1)  // keep the row-scaled entries in LDS for the tiles
+            for (int i = 0; i < k; i++)
+                Mt[t * k + i] = mulm(Mt[t * k + i], sc);
+    }
     if (L.KS()) {
-        // the matrix-core operand tiles, from the `plain` rows just written
-        __threadfence_block();
+        // the matrix-core operand tiles, from the row-scaled entries in LDS
         __syncthreads();
-        for (size_t d = tid; d < L.mf_words(); d += 64)
-            mat[L.mf() + d] = pack_mf_dword(L, mat, d);
+        const int32_t* rows = reinterpret_cast<const int32_t*>(Mt);
+        for (size_t d = tid; d < L.mf_words(); d += NT)
+            mat[L.mf() + d] = pack_mf_dword(L, rows, d);
     }
 }
 
@@ -1499,9 +1509,14 @@ int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
         return -3;
     Oor none{nullptr, nullptr, 0, 0};
     const size_t lds = static_cast<size_t>(k) * k * 4 * (mode ? 2 : 1);
-    hipLaunchKernelGGL(decode_ctx_kernel, dim3(S), dim3(64), lds, st, k, r, mode,
-                       L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                       slot_base, by_pos, words);
+    if (k > 32)
+        hipLaunchKernelGGL(decode_ctx_kernel<256>, dim3(S), dim3(256), lds, st, k, r,
+                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
+                           slot_base, by_pos, words);
+    else
+        hipLaunchKernelGGL(decode_ctx_kernel<64>, dim3(S), dim3(64), lds, st, k, r,
+                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
+                           slot_base, by_pos, words);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

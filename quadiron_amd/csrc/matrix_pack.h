@@ -80,8 +80,9 @@ QI_HD void split_i8(uint32_t c, int32_t& a, int32_t& b)
 // Pack row t (kin canonical entries) of the block.  Rows holding a
 // coefficient that breaks coef_ok are scaled by a unit s first and the
 // result is multiplied back by s^-1 (rscale, also |s^-1| <= 32766).
-QI_HD void pack_row(const uint32_t* row, const MatLayout& L, int t,
-                    int32_t* block)
+// Returns the row scale s (1 = unscaled).
+QI_HD uint32_t pack_row(const uint32_t* row, const MatLayout& L, int t,
+                        int32_t* block)
 {
     const int kin = L.kin, KP = L.KP;
     // s = 1 almost always (a row needs scaling with probability ~ 5 kin /
@@ -121,6 +122,7 @@ QI_HD void pack_row(const uint32_t* row, const MatLayout& L, int t,
     block[L.rscale() + t] = s == 1 ? 1 : balanced(powmod_c(s, 65535u));
     if (L.KS())
         block[L.kmf() + t] = static_cast<int32_t>(mulmod_c(sq, 32896u));
+    return s;
 }
 
 // Dword d of the MFMA operand tiles, from the `plain` rows pack_row wrote.
@@ -131,18 +133,20 @@ QI_HD void pack_row(const uint32_t* row, const MatLayout& L, int t,
 //   ty 0: [a | 0]   ty 1: [0 | b]   ty 2: [b | a]       (c = 256 a + b)
 // i.e. D0 = sum a h', D1 = sum b l', D2 = sum (b h' + a l') and
 // sum c x = 256 D2 + D1 - D0 + 32896 sum c  (2^16 = -1 mod q).
-QI_HD int32_t pack_mf_dword(const MatLayout& L, const int32_t* block, size_t d)
+// `rows`: the row-scaled canonical entries, kin per row (the block's
+// `plain` section, or a copy of it in LDS).
+QI_HD int32_t pack_mf_dword(const MatLayout& L, const int32_t* rows, size_t d)
 {
-    const int KS = L.KS(), KH = 16 * KS;
-    const size_t tile = d / 128;
-    const int rem = static_cast<int>(d % 128), lane = rem / 2, dw = rem % 2;
-    const int ty = static_cast<int>(tile % 3);
-    const int ks = static_cast<int>((tile / 3) % static_cast<size_t>(KS));
-    const int rb = static_cast<int>(tile / (3 * static_cast<size_t>(KS)));
+    const int KS = L.KS(), KH = 16 * KS;  // KS is 1, 2 or 4
+    const int sh = KS == 1 ? 0 : KS == 2 ? 1 : 2;
+    const int tile = static_cast<int>(d >> 7);
+    const int rem = static_cast<int>(d & 127), lane = rem >> 1, dw = rem & 1;
+    const int ty = tile % 3, rk = tile / 3;
+    const int ks = rk & (KS - 1), rb = rk >> sh;
     const int t = 16 * rb + (lane & 15), g = lane >> 4;
     if (t >= L.R)
         return 0;
-    const int32_t* plain = block + L.plain() + static_cast<size_t>(t) * L.kin;
+    const int32_t* plain = rows + static_cast<size_t>(t) * L.kin;
     uint32_t v = 0;
     for (int jb = 0; jb < 4; jb++) {
         const int K = 32 * ks + 8 * g + 4 * dw + jb;

@@ -69,7 +69,7 @@ void pack_matrix(const MatLayout& L, const uint32_t* M, int32_t* block)
     for (int t = 0; t < L.R; t++)
         pack_row(M + static_cast<size_t>(t) * L.kin, L, t, block);
     for (size_t d = 0; d < L.mf_words(); d++)
-        block[L.mf() + d] = pack_mf_dword(L, block, d);
+        block[L.mf() + d] = pack_mf_dword(L, block + L.plain(), d);
 }
 
 }  // namespace qi

@@ -181,7 +181,7 @@ static void test_matrix_mfma(std::mt19937_64& g)
             for (int t = 0; t < R; t++)
                 pack_row(M.data() + static_cast<size_t>(t) * kin, L, t, blk.data());
             for (size_t d = 0; d < L.mf_words(); d++)
-                blk[L.mf() + d] = pack_mf_dword(L, blk.data(), d);
+                blk[L.mf() + d] = pack_mf_dword(L, blk.data() + L.plain(), d);
             const int KS = L.KS(), KH = 16 * KS;
             auto opb = [&](int rb, int ks, int ty, int lane, int j) {
                 const size_t dw = L.mf() +

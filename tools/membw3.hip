@@ -195,7 +195,10 @@ int main(int argc, char** argv)
     printf("--- rep %d\n", rep);
     RUN(256, 0, 1, 0, 2)
     RUN(256, 3, 1, 0, 18)
-    RUN(256, 3, 2, 0, 18)
+    RUN(512, 3, 1, 0, 18)
+    RUN(1024, 3, 1, 0, 18)
+    RUN(512, 3, 2, 0, 18)
+    RUN(1024, 3, 2, 0, 18)
 #define SPLIT(ORD, SA)                                                            \
     {                                                                             \
         const int tiles = P / 128;                                                \
