@@ -1,6 +1,7 @@
 // Plan construction and host-side matrix math for the RS-FNT engine.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -12,6 +13,14 @@
 #include "qi_plan.h"
 
 namespace qi {
+
+// QI_ENC_MATRIX=1 sends non-systematic encodes with K <= 64 through the
+// matrix-core kernel instead of the register FNT codelets (A/B knob)
+static bool enc_matrix_forced()
+{
+    const char* e = std::getenv("QI_ENC_MATRIX");
+    return e && e[0] == '1';
+}
 
 static uint32_t addm(uint32_t a, uint32_t b)
 {
@@ -123,7 +132,7 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
     const int kp = matrix_kp(k);
     if (kp < 0) {
         ok = false;  // k > 64 is not supported by the matrix kernel
-    } else if (p->sys || p->K > 64) {
+    } else if (p->sys || p->K > 64 || enc_matrix_forced()) {
         MatLayout L{p->n_outputs, k, kp};
         std::vector<uint32_t> M;
         if (p->sys) {

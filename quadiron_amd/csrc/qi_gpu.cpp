@@ -103,7 +103,7 @@ int qi_gpu_encode(qi_plan* p, const uint16_t* d_data, long long dss,
         return 0;
     Oor oor{d_counts, d_entries, p->n_outputs, cap};
     RowDst out{d_out, oss, ors};
-    if (!p->sys && p->K <= 64)
+    if (!p->d_gen)
         return launch_encode_fnt(p->k, p->n, p->n_outputs, p->d_twist, d_data,
                                  dss, drs, out, words, n_stripes, oor,
                                  p->d_err, st(stream));
