@@ -848,9 +848,18 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
         kt = t < L.R ? kmf[t] : 0;
         rs = t < L.R ? rscale[t] : 1;
     };
+    // tall matrices (RB >= waves per block, the encode generators): wave wv
+    // takes row blocks wv, wv + 4, ... over all the block's super tiles, so
+    // each wave fetches only its own operand tiles (4x fewer L2 operand
+    // reads than every wave walking every row block); otherwise every wave
+    // takes every row block over its own COLS super tiles
+    constexpr int NW = kBlock / 64;
+    const bool rsplit = RB >= NW;  // uniform
+    const int rb0 = rsplit ? wv : 0, rbs = rsplit ? NW : 1;
+    const int nst = rsplit ? NW * COLS : COLS;
     qi_v2i bop[KS][3];
     int32_t kt, rs;
-    load_ops(0, bop, kt, rs);
+    load_ops(rb0, bop, kt, rs);
 
     // stage the tile as byte planes h' (rows 0..KH-1) and l' (rows KH..),
     // all row loads issued back to back; rows past kin load a clamped row
@@ -931,15 +940,15 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
     // change the address space)
     auto* lds = (__attribute__((address_space(3))) uint8_t*)img;
     const uint32_t abase = static_cast<uint32_t>((8 * g + q) * RSB + 8 * p);
-    for (int rb = 0; rb < RB; rb++) {
+    for (int rb = rb0; rb < RB; rb += rbs) {
         const int t = 16 * rb + tl;
         const bool trow = t < L.R;
         qi_v2i bnx[KS][3];
         int32_t ktn = 0, rsn = 1;
-        if (rb + 1 < RB)
-            load_ops(rb + 1, bnx, ktn, rsn);
-        for (int st = 0; st < COLS; st++) {
-            const int ST = wv * COLS + st;
+        if (rb + rbs < RB)
+            load_ops(rb + rbs, bnx, ktn, rsn);
+        for (int st = 0; st < nst; st++) {
+            const int ST = rsplit ? st : wv * COLS + st;
             qi_v4i acc[4][3];
 #pragma unroll
             for (int T = 0; T < 4; T++) {
@@ -1062,7 +1071,7 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
-        if (rb + 1 < RB) {
+        if (rb + rbs < RB) {
 #pragma unroll
             for (int ks = 0; ks < KS; ks++)
 #pragma unroll
