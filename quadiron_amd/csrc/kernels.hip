@@ -955,17 +955,37 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                 acc[T][0] = qi_v4i{0, 0, 0, 0};
                 acc[T][1] = qi_v4i{kt, kt, kt, kt};
                 acc[T][2] = qi_v4i{0, 0, 0, 0};
-#pragma unroll
-                for (int ks = 0; ks < KS; ks++) {
+                auto rd_a = [&](int ks) {
                     auto* pa = (__attribute__((address_space(3))) qi_v2i*)(
                         lds + abase + 32 * ks * RSB + (4 * ST + T) * 16);
-                    const long a = __builtin_bit_cast(
-                        long, __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa));
+                    return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
+                };
+                if constexpr (KS == 1) {
+                    const long a = __builtin_bit_cast(long, rd_a(0));
 #pragma unroll
                     for (int ty = 0; ty < 3; ty++)
                         acc[T][ty] = __builtin_amdgcn_mfma_i32_16x16x32_i8(
-                            a, __builtin_bit_cast(long, bop[ks][ty]), acc[T][ty], 0,
+                            a, __builtin_bit_cast(long, bop[0][ty]), acc[T][ty], 0,
                             0, 0);
+                } else {
+                    // two K-steps per v_mfma_i32_16x16x64_i8 (CDNA4: the
+                    // cycles of 16x16x32_i8 at twice the K).  Lane l holds
+                    // the 8 A bytes of steps ks and ks + 1 (and the same
+                    // two B halves): A and B share their lane/byte -> K
+                    // map, so the 64-K product is the sum of the two
+                    // 32-K products whatever that map is
+#pragma unroll
+                    for (int ks = 0; ks < KS; ks += 2) {
+                        const qi_v2i a0 = rd_a(ks), a1 = rd_a(ks + 1);
+                        const qi_v4i a{a0.x, a0.y, a1.x, a1.y};
+#pragma unroll
+                        for (int ty = 0; ty < 3; ty++) {
+                            const qi_v4i b{bop[ks][ty].x, bop[ks][ty].y,
+                                           bop[ks + 1][ty].x, bop[ks + 1][ty].y};
+                            acc[T][ty] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                                a, b, acc[T][ty], 0, 0, 0);
+                        }
+                    }
                 }
             }
             // epilogue: lane (g, t) holds row t, columns cb .. cb + 15;
