@@ -980,6 +980,12 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                         const qi_v4i a{a0.x, a0.y, a1.x, a1.y};
 #pragma unroll
                         for (int ty = 0; ty < 3; ty++) {
+                            // [a | 0] is zero over the l' half of K and
+                            // [0 | b] over the h' half: skip the pairs
+                            // that lie in a zero half (KS = 4)
+                            if ((ty == 0 && ks >= KS / 2) ||
+                                (ty == 1 && ks + 1 < KS / 2))
+                                continue;
                             const qi_v4i b{bop[ks][ty].x, bop[ks][ty].y,
                                            bop[ks + 1][ty].x, bop[ks + 1][ty].y};
                             acc[T][ty] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
