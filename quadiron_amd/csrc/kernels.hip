@@ -1152,6 +1152,70 @@ __device__ __forceinline__ uint32_t powm(uint32_t b, uint32_t e)
 // NT threads: the Lagrange part runs on the first wave (lane = point); the
 // row packing and the MFMA operand tiles use every thread (NT = 256 for
 // k > 32, where they dominate and there are few stripes per launch)
+// pack_row (matrix_pack.h) on a group of 4 adjacent lanes, lane `sub`
+// taking entries sub, sub + 4, ...: the same row scale search (uniform in
+// the group), packed pairs, canonical `plain` entries, kcorr / rscale / kmf,
+// and the row-scaled entries written back to the LDS row for the tiles
+__device__ __forceinline__ uint32_t g4_or(uint32_t v)
+{
+    v |= __shfl_xor(v, 1, 4);
+    return v | __shfl_xor(v, 2, 4);
+}
+__device__ __forceinline__ uint32_t g4_add(uint32_t v)
+{
+    v += __shfl_xor(v, 1, 4);
+    return v + __shfl_xor(v, 2, 4);
+}
+__device__ void pack_row_g4(uint32_t* row, const MatLayout& L, int t,
+                            int32_t* block, int sub)
+{
+    const int kin = L.kin, KP = L.KP;
+    uint32_t bad = 0;
+    for (int i = sub; i < kin; i += 4)
+        bad |= !coef_ok(balanced(row[i]));
+    bad = g4_or(bad);
+    uint32_t s = 1;
+    while (bad) {  // rare; s, si and bad are uniform in the group
+        s++;
+        const int32_t si = balanced(powm(s, 65535u));
+        if (iabs32(si) > 32766)
+            continue;
+        bad = 0;
+        for (int i = sub; i < kin; i += 4)
+            bad |= !coef_ok(balanced(mulm(row[i], s)));
+        bad = g4_or(bad);
+    }
+    int32_t* packed = block + static_cast<size_t>(t) * KP;
+    int32_t* plain = block + L.plain();
+    for (int j = sub; j < KP; j += 4) {
+        int32_t lo = 0, hi = 0;
+        if (2 * j < kin)
+            lo = balanced(s == 1 ? row[2 * j] : mulm(row[2 * j], s));
+        if (2 * j + 1 < kin)
+            hi = balanced(s == 1 ? row[2 * j + 1] : mulm(row[2 * j + 1], s));
+        packed[j] = static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xffffu) |
+                                         (static_cast<uint32_t>(hi) << 16));
+    }
+    uint32_t sum = 0;  // <= 64 * 65536
+    for (int i = sub; i < kin; i += 4) {
+        const uint32_t c = s == 1 ? row[i] : mulm(row[i], s);
+        plain[static_cast<size_t>(t) * kin + i] = static_cast<int32_t>(c);
+        row[i] = c;
+        sum += c;
+    }
+    sum = g4_add(sum);
+    if (sub == 0) {
+        const uint32_t sq = sum % 65537u;
+        block[L.kcorr() + t] = static_cast<int32_t>(mulm(sq, 32768u));
+        block[L.rscale() + t] = s == 1 ? 1 : balanced(powm(s, 65535u));
+        if (L.KS())
+            block[L.kmf() + t] = static_cast<int32_t>(mulm(sq, 32896u));
+    }
+}
+
+#ifndef QI_CTX_SKIP
+#define QI_CTX_SKIP 0  // timing probe only: skip context phases (wrong results)
+#endif
 template <int NT>
 __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
@@ -1222,9 +1286,11 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         // 1 / A'(x_i) = 1 / prod_{j != i} (x_i - x_j)
         const uint32_t xi = xs[tid];
         uint32_t den = 1;
+#if !(QI_CTX_SKIP & 4)
         for (int j = 0; j < k; j++)
             if (j != tid)
                 den = mulm(den, subm(xi, xs[j]));
+#endif
         const uint32_t inv = powm(den, 65535u);
         // Q_i = A / (x - x_i) by synthetic division from the top
         uint32_t q = 1;  // A[k]
@@ -1248,18 +1314,45 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         }
     }
     __syncthreads();
-    for (int t = tid; t < L.R; t += NT) {
-        const uint32_t sc = pack_row(Mt + t * k, L, t, mat);
-        if (sc != 1)  // keep the row-scaled entries in LDS for the tiles
-            for (int i = 0; i < k; i++)
-                Mt[t * k + i] = mulm(Mt[t * k + i], sc);
-    }
+    // 4 lanes per row: pack_row's work split over the row's entries, its
+    // reductions over the 4 lanes (k = 64: 92 -> 62 us per 1024 stripes)
+    for (int t = tid / 4; t < ((QI_CTX_SKIP & 1) ? 0 : L.R); t += NT / 4)
+        pack_row_g4(Mt + t * k, L, t, mat, tid & 3);
     if (L.KS()) {
         // the matrix-core operand tiles, from the row-scaled entries in LDS
         __syncthreads();
         const int32_t* rows = reinterpret_cast<const int32_t*>(Mt);
-        for (size_t d = tid; d < L.mf_words(); d += NT)
-            mat[L.mf() + d] = pack_mf_dword(L, rows, d);
+        // per (row t, 4 consecutive entries): split once, then place the
+        // a / b byte words in their 6 tile dwords (pack_mf_dword's layout,
+        // zeros included; rows t >= R are zero)
+        const int KS = L.KS(), KH = 16 * KS, RBp = L.RB() * 16;
+        int32_t* mf = mat + L.mf();
+        for (int it = tid; it < ((QI_CTX_SKIP & 2) ? 0 : RBp * (KH / 4)); it += NT) {
+            const int t = it / (KH / 4), i0 = 4 * (it % (KH / 4));
+            uint32_t aw = 0, bw = 0;
+            if (t < L.R) {
+#pragma unroll
+                for (int jb = 0; jb < 4; jb++) {
+                    if (i0 + jb < k) {
+                        int32_t a, b;
+                        split_i8(static_cast<uint32_t>(rows[t * k + i0 + jb]), a, b);
+                        aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
+                        bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
+                    }
+                }
+            }
+            const int rb = t >> 4, tl4 = t & 15;
+#pragma unroll
+            for (int half = 0; half < 2; half++) {
+                const int K = half * KH + i0;
+                const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
+                const size_t base =
+                    static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl4) * 2 + dw;
+                mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
+                mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
+                mf[base + 256] = static_cast<int32_t>(half ? aw : bw);  // [b | a]
+            }
+        }
     }
 }
 
