@@ -256,6 +256,18 @@ def test_batch_vs_oracle(k, m, sys_, S, P):
                      n_craft=16 if k <= 64 else 0)
 
 
+@pytest.mark.parametrize("k,m,S,P", [
+    (16, 48, 3, 4096),        # 64 x 16 generator, KS = 1
+    (33, 31, 2, 2048),        # KS = 4 with padded inputs (x64 MFMA, zero K halves)
+    (64, 960, 2, 2048),       # cfg3 generator, row blocks split over waves
+])
+def test_matrix_encode_knob_vs_oracle(monkeypatch, k, m, S, P):
+    """QI_ENC_MATRIX=1 (read at plan creation) sends non-systematic encodes
+    through the matrix-core kernel: the A/B path must stay bit-exact too."""
+    monkeypatch.setenv("QI_ENC_MATRIX", "1")
+    _batch_roundtrip(k, m, 0, S, P, seed=7 * k + m + P, n_craft=16)
+
+
 def test_cfg2_full_size_roundtrip():
     """BASELINE cfg2 geometry (k=16, n=64, 64 KiB packets) at 32 stripes:
     encode -> per-stripe random erasures -> decode == data, and stripe 0
