@@ -122,6 +122,10 @@ __device__ __forceinline__ void block_map(int b, int tiles, int& s, int& tile)
 #ifndef QI_ENC_PAIR
 #define QI_ENC_PAIR 0
 #endif
+// waves per SIMD the K = 64 encode body is compiled for (A/B knob)
+#ifndef QI_ENC_K64_WAVES
+#define QI_ENC_K64_WAVES 2
+#endif
 #ifndef QI_ENC_RELOAD_MASK
 #define QI_ENC_RELOAD_MASK (1 << 5)
 #endif
@@ -440,7 +444,7 @@ __device__ __forceinline__ void encode_body(
 template <int K, int COLS, bool KEQ, bool BUF>
 // 4 waves per SIMD: the K=16, COLS=2 body fits 128 VGPRs without spills or
 // extra instructions (3 waves at the compiler's default 130)
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 64 ? 2 : 4))) void
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 64 ? QI_ENC_K64_WAVES : 4))) void
 encode_fnt_kernel(
     int k, int n, int n_out, const int32_t* __restrict__ twist,
     const uint16_t* __restrict__ data, long long dss, uint32_t irs,
