@@ -868,7 +868,9 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
     // stage the tile as byte planes h' (rows 0..KH-1) and l' (rows KH..),
     // all row loads issued back to back; rows past kin load a clamped row
     // (their operand bytes are 0)
-    uint32_t w[KH][COLS / 2];
+    // COLS = 1: one u16 column per lane (256-column blocks: half the LDS
+    // image, for the KS = 4 kernels' occupancy)
+    uint32_t w[KH][COLS > 1 ? COLS / 2 : 1];
 #pragma unroll
     for (int i = 0; i < KH; i++) {
         const int ii = i < kin ? i : kin - 1;
@@ -878,7 +880,11 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
         g.r = lo ? g0.r : g1.r;
         const uint32_t off = static_cast<uint32_t>(
             lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
-        ld_dw<COLS / 2, true, kAuxLd>(g, off, voff, w[i]);
+        if constexpr (COLS == 1)
+            w[i][0] = __builtin_amdgcn_raw_buffer_load_b16(
+                g.r, static_cast<int>(voff), static_cast<int>(off), kAuxLd);
+        else
+            ld_dw<COLS / 2, true, kAuxLd>(g, off, voff, w[i]);
     }
     const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) +
                           4 * ((cl % 64) / 16) + cl % 4;
@@ -892,6 +898,9 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                 __builtin_amdgcn_perm(w[i][1], w[i][0], 0x06040200u) ^ 0x80808080u;
             *reinterpret_cast<uint32_t*>(img + i * RSB + lpos) = hi;
             *reinterpret_cast<uint32_t*>(img + (KH + i) * RSB + lpos) = lo;
+        } else if constexpr (COLS == 1) {
+            img[i * RSB + lpos] = static_cast<uint8_t>((w[i][0] >> 8) ^ 0x80u);
+            img[(KH + i) * RSB + lpos] = static_cast<uint8_t>(w[i][0] ^ 0x80u);
         } else {
             const uint32_t hi =
                 __builtin_amdgcn_perm(0u, w[i][0], 0x0c0c0301u) ^ 0x8080u;
@@ -1532,6 +1541,11 @@ static int mat_dispatch(int cols, const MatLayout& L, const int32_t* mat,
 #endif
 // columns per thread of the KS = 1 matrix-core kernel (4: 1024-column
 // blocks, 35 KB LDS; 2: 512-column blocks, 19 KB LDS, more blocks per CU)
+// columns per lane of the KS = 4 (k > 32) kernel: 2 (512-column blocks,
+// 77 KB LDS, 2 blocks/CU) or 1 (256 columns, 44 KB, 3 blocks/CU)
+#ifndef QI_MFMA_COLS4
+#define QI_MFMA_COLS4 2
+#endif
 #ifndef QI_MFMA_COLS1
 #define QI_MFMA_COLS1 4
 #endif
@@ -1602,7 +1616,7 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
             rc = mfma_launch<2, 2>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
                                    S, io, slot_base, oo, route, rstride, err, st);
         else
-            rc = mfma_launch<4, 2>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
+            rc = mfma_launch<4, QI_MFMA_COLS4>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
                                    S, io, slot_base, oo, route, rstride, err, st);
         if (rc || wfull == words)
             return rc;
