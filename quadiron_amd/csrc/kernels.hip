@@ -89,6 +89,11 @@ struct Region {
 #endif
 constexpr int kAuxLd = QI_AUX_LD;
 constexpr int kAuxSt = QI_AUX_ST;
+// cache policy of the matrix-core kernel's whole-line output stores
+#ifndef QI_AUX_ST_MF
+#define QI_AUX_ST_MF QI_AUX_ST
+#endif
+constexpr int kAuxStMf = QI_AUX_ST_MF;
 
 // XCD-aware block -> (stripe, tile) map.  Workgroups are dispatched
 // round-robin over the 8 XCDs (block b runs on XCD b % 8), so with the plain
@@ -1102,7 +1107,7 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                         static_cast<uint32_t>(ot) * ors +
                         static_cast<uint32_t>((col0 + 64 * ST + 8 * c) * 2);
                     __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo),
-                                                           0, kAuxSt);
+                                                           0, kAuxStMf);
                 }
             }
             // the staging tile is rewritten by the next (ST, rb): keep this
