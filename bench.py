@@ -9,13 +9,24 @@ Inputs are resident in HBM before the timed region starts.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--stripes S]
 
-For N > 1 launch one process per GPU (torch.distributed.run); stripes shard
-across ranks with no data-path collective (weak scaling: S stripes per GPU).
-Rank 0 prints ONE JSON line.
+Multi-GPU: one process per GPU.  Stripes are independent codewords, so every
+rank encodes/decodes its own batch of S stripes with no data-path collective
+(weak scaling, the reference bench's per-thread replica model,
+benchmark/benchmark.cpp:813-817).  Either launch the ranks yourself
+(`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`) or
+run `python bench.py --gpus N`: the process then starts torch.distributed.run
+itself, as a child, before anything touches the GPU.  `--gpus` must match the
+world size the ranks see; a mismatch is an error, never a silent 1-GPU run.
+Rank 0 prints ONE JSON line; `n_gpus` is the process group's size.
+
+`--dry-run` runs the same launch / shard / reduce / report logic on the CPU
+(gloo, no HIP calls, no kernels): tests/test_distributed.py drives it.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,7 +36,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import quadiron_amd as qa  # noqa: E402
+import quadiron_amd as qa  # noqa: E402  (loads no library until used)
 
 K_DATA, M_PAR, PKT_BYTES = 16, 48, 65536
 # BASELINE.json configs measurable on one GPU: (k, m, packet bytes, stripes).
@@ -48,36 +59,101 @@ def alg_bytes(k, m, P, systematic=False):
     return enc_rows * 2 * P, 2 * k * 2 * P
 
 
-def cpu_baseline(k, m, P, threads, stripes_per_thread, systematic=False):
-    """QuadIron's own AVX2 path (oracle/_ref/libqiref_avx2.so, compiled from
-    the reference sources) timed on this host: `threads` independent replicas
-    (the reference bench's -g model) each encoding + decoding
-    `stripes_per_thread` stripes of k x 64 KiB, one fixed n-k erasure
-    pattern.  Falls back to the plain-C oracle port when the reference build
-    is absent."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_share():
+    """Host threads this process may use: the box's CPU share (OMP_NUM_THREADS
+    is set to it on the GPU boxes), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _ref_leg(lib, k, m, P, threads, seconds, systematic, missing):
     import ctypes as C
-    ref = os.path.join(ROOT, "oracle", "_ref", "libqiref_avx2.so")
     enc_b, dec_b = alg_bytes(k, m, P, systematic)
+    stripes = C.c_longlong()
+    wall = lib.ref_bench(int(systematic), k, m, C.c_size_t(P), C.c_double(seconds),
+                         threads, missing.ctypes.data_as(C.c_void_p),
+                         C.byref(stripes), None, None)
+    n = stripes.value
+    return {"value": n * (enc_b + dec_b) / wall / 1e9, "unit": "GB/s",
+            "cores": threads, "stripes": n, "wall_s": round(wall, 3)}
+
+
+def _port_leg(k, m, P, seconds, systematic, missing):
+    """The plain-C oracle (a scalar restatement, one thread) when the
+    reference build is absent."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from qi_testlib import oracle_decode_blocks, oracle_encode_blocks
+    enc_b, dec_b = alg_bytes(k, m, P, systematic)
+    rng = np.random.default_rng(1)
+    data = rng.integers(0, 256, (k, 2 * P), dtype=np.uint8)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        outs, oor, cnt = oracle_encode_blocks(k, m, systematic, data)
+        oracle_decode_blocks(k, m, systematic, outs, oor, cnt, missing, data)
+        n += 1
+        wall = time.perf_counter() - t0
+        if wall >= seconds:
+            break
+    return {"value": n * (enc_b + dec_b) / wall / 1e9, "unit": "GB/s",
+            "cores": 1, "stripes": n, "wall_s": round(wall, 3)}
+
+
+def cpu_baseline(k, m, P, systematic=False, seconds=1.0, threads=None):
+    """QuadIron's own AVX2 path (oracle/_ref/libqiref_avx2.so, compiled from
+    the reference sources; ref_driver.cpp ref_bench) timed on this host on
+    the same stripes: independent per-thread replicas (benchmark.cpp:813-817)
+    each encoding + decoding one stripe at a time from one fixed n-k erasure
+    pattern for >= `seconds` of wall time, on 1 thread and on every thread of
+    this process's CPU share.  Falls back to the plain-C oracle (1 thread,
+    kind "port") when the reference build is absent."""
+    import ctypes as C
+    rng = np.random.default_rng(1)
+    missing = np.zeros(k + m, np.int32)
+    missing[rng.choice(k + m, m, replace=False)] = 1
+    threads = threads or cpu_share()
+    ref = os.path.join(ROOT, "oracle", "_ref", "libqiref_avx2.so")
+    name = (f"RS-FNT{'-sys' if systematic else ''} k={k} m={m} "
+            f"pkt={2 * P // 1024}KiB")
     if os.path.exists(ref):
         lib = C.CDLL(ref)
         lib.ref_bench.restype = C.c_double
-        rng = np.random.default_rng(1)
-        missing = np.zeros(k + m, np.int32)
-        missing[rng.choice(k + m, m, replace=False)] = 1
-        e = C.c_double()
-        d = C.c_double()
-        wall = lib.ref_bench(int(systematic), k, m, C.c_size_t(P), stripes_per_thread,
-                             threads, missing.ctypes.data_as(C.c_void_p),
-                             C.byref(e), C.byref(d))
-        total = threads * stripes_per_thread * (enc_b + dec_b)
-        return {"value": total / wall / 1e9, "unit": "GB/s", "cores": threads,
-                "kind": "reference",
-                "sample": f"{threads} threads x {stripes_per_thread} stripes "
-                          f"of RS-FNT{'-sys' if systematic else ''} k={k} "
-                          f"m={m} pkt={2 * P // 1024}KiB enc+dec "
-                          f"(QuadIron AVX2 build, pkt_size {P} words), "
-                          f"wall {wall:.2f}s"}
-    return None
+        lib.ref_bench.argtypes = [C.c_int, C.c_int, C.c_int, C.c_size_t,
+                                  C.c_double, C.c_int, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p]
+        one = _ref_leg(lib, k, m, P, 1, seconds, systematic, missing)
+        allc = _ref_leg(lib, k, m, P, threads, seconds, systematic, missing)
+        kind = "reference"
+        what = f"QuadIron AVX2 build (oracle/_ref), pkt_size {P} words"
+    else:
+        one = _port_leg(k, m, P, seconds, systematic, missing)
+        allc = dict(one)
+        kind = "port"
+        what = "plain-C oracle restatement, scalar, 1 thread"
+    return {"value": allc["value"], "unit": "GB/s", "cores": allc["cores"],
+            "kind": kind,
+            "sample": f"{name} enc+dec one stripe at a time per thread, "
+                      f"fixed n-k erasure pattern, >= {seconds:g} s per leg: "
+                      f"{allc['stripes']} stripes on {allc['cores']} threads "
+                      f"in {allc['wall_s']} s, {one['stripes']} stripes on 1 "
+                      f"thread in {one['wall_s']} s ({what})",
+            "all_cores": allc, "one_core": one,
+            "cpu": cpu_model(), "host_cpus": os.cpu_count()}
 
 
 def shard(rank, world, stripes_per_gpu):
@@ -103,7 +179,25 @@ def aggregate_value(world, stripes_per_gpu, steps, k, m, P, elapsed,
     return world * stripes_per_gpu * steps * (enc_b + dec_b) / elapsed / 1e9
 
 
-def main():
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Start `n` ranks of this script under torch.distributed.run as a child
+    process and return its exit code.  The caller has not initialised HIP
+    (nothing here touches the GPU), so no process is replaced."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -114,21 +208,51 @@ def main():
     ap.add_argument("--chunks", type=int, default=1)
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-stripes", type=int, default=200)
-    args = ap.parse_args()
+    ap.add_argument("--cpu-seconds", type=float, default=1.0)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch/shard/reduce/report on the CPU (gloo), no "
+                         "HIP calls: tests the multi-rank path without GPUs")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus, argv))
+        world_env = 1
+    else:
+        world_env = int(env_world)
+        if world_env != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}: "
+                     "launch one process per GPU with matching sizes")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dry = args.dry_run
+
     dist = None
-    if world > 1:
+    if world_env > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dry:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl",
+                                    device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
+        rank = dist.get_rank()
     else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+        world = 1
+    if dry:
+        dev = torch.device("cpu")
+    else:
+        if world == 1:
+            torch.cuda.set_device(0)
+        dev = torch.device("cuda", torch.cuda.current_device())
 
     k, m, pkt_bytes, S = CONFIGS[args.cfg]
     if args.stripes:
@@ -136,89 +260,118 @@ def main():
     P = pkt_bytes // 2
     sys_ = bool(args.systematic)
     headline = args.cfg == "cfg2" and not sys_
-    plan = qa.Plan(k, m, sys_)
-    n_out = plan.n_outputs
-    cap = 64
-    g = torch.Generator(device=dev)
+    n = 1
+    while n < k + m:
+        n *= 2
     lo, _ = shard(rank, world, S)
-    g.manual_seed(0x51D00001 + lo)  # this rank's shard of the global batch
-    data = torch.randint(-32768, 32768, (S, k, P), dtype=torch.int16,
-                         device=dev, generator=g)
-    coded = torch.empty((S, n_out, P), dtype=torch.int16, device=dev)
-    dec = torch.empty((S, k, P), dtype=torch.int16, device=dev)
-    counts = torch.zeros(S * n_out, dtype=torch.int32, device=dev)
-    entries = torch.zeros(S * n_out * cap, dtype=torch.int32, device=dev)
-    # per-stripe erasure pattern: keep a random k-subset of the n ids
-    perm = torch.rand((S, k + m), device=dev, generator=g).argsort(dim=1)
-    ids = perm[:, :k].sort(dim=1).values.to(torch.int16).contiguous()
-    ctx = torch.empty(plan.ctx_bytes(S, P), dtype=torch.uint8, device=dev)
-    # the batch is processed as `chunks` slices round-robin over `streams`
-    # HIP streams, so one slice's encode (write-heavy) overlaps another's
-    # decode (read-heavy); every slice is still encoded, erased and decoded
-    # inside the timed step
     NC = max(1, args.chunks)
     assert S % NC == 0, "stripes must divide into chunks"
     C = S // NC
-    streams = ([torch.cuda.current_stream()] if NC == 1 else
-               [torch.cuda.Stream() for _ in range(max(1, args.streams))])
-    cstride = plan.ctx_bytes(1, P)
-
     ev = []
 
-    def step(timed):
-        for j in range(NC):
-            st = streams[j % len(streams)]
-            a, b = j * C, (j + 1) * C
-            with torch.cuda.stream(st):
-                cnt = counts[a * n_out:b * n_out]
-                ent = entries[a * n_out * cap:b * n_out * cap]
-                cx = ctx[a * cstride:b * cstride]
-                cnt.zero_()
-                if timed:
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e2 = torch.cuda.Event(enable_timing=True)
-                    e0.record(st)
-                plan.encode(data[a:b], coded[a:b], cnt, ent, cap,
-                            stream=st.cuda_stream)
-                if timed:
-                    e1.record(st)
-                plan.decode_ctx(ids[a:b], cx, P, cnt, ent, cap,
+    if dry:
+        # the same loop structure on a small CPU stand-in per step
+        n_out = n
+        data = torch.zeros((NC, 1024), dtype=torch.int64)
+        data += lo
+
+        def step(timed):
+            for j in range(NC):
+                data[j] = (data[j] * 3 + 1) % 65537
+
+        def check():
+            return True
+        streams = [None]
+    else:
+        plan = qa.Plan(k, m, sys_)
+        n_out = plan.n_outputs
+        cap = 64
+        g = torch.Generator(device=dev)
+        g.manual_seed(0x51D00001 + lo)  # this rank's shard of the global batch
+        data = torch.randint(-32768, 32768, (S, k, P), dtype=torch.int16,
+                             device=dev, generator=g)
+        coded = torch.empty((S, n_out, P), dtype=torch.int16, device=dev)
+        dec = torch.empty((S, k, P), dtype=torch.int16, device=dev)
+        counts = torch.zeros(S * n_out, dtype=torch.int32, device=dev)
+        entries = torch.zeros(S * n_out * cap, dtype=torch.int32, device=dev)
+        # per-stripe erasure pattern: keep a random k-subset of the n ids
+        perm = torch.rand((S, k + m), device=dev, generator=g).argsort(dim=1)
+        ids = perm[:, :k].sort(dim=1).values.to(torch.int16).contiguous()
+        ctx = torch.empty(plan.ctx_bytes(S, P), dtype=torch.uint8, device=dev)
+        # the batch is processed as `chunks` slices round-robin over
+        # `streams` HIP streams, so one slice's encode (write-heavy) overlaps
+        # another's decode (read-heavy); every slice is still encoded,
+        # erased and decoded inside the timed step
+        streams = ([torch.cuda.current_stream()] if NC == 1 else
+                   [torch.cuda.Stream() for _ in range(max(1, args.streams))])
+        cstride = plan.ctx_bytes(1, P)
+
+        def step(timed):
+            for j in range(NC):
+                st = streams[j % len(streams)]
+                a, b = j * C, (j + 1) * C
+                with torch.cuda.stream(st):
+                    cnt = counts[a * n_out:b * n_out]
+                    ent = entries[a * n_out * cap:b * n_out * cap]
+                    cx = ctx[a * cstride:b * cstride]
+                    cnt.zero_()
+                    if timed:
+                        # HIP events on the launch stream itself
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e2 = torch.cuda.Event(enable_timing=True)
+                        e0.record(st)
+                    plan.encode(data[a:b], coded[a:b], cnt, ent, cap,
                                 stream=st.cuda_stream)
-                plan.decode(cx, ids[a:b], coded[a:b], dec[a:b], data=data[a:b],
-                            counts=cnt, entries=ent, cap=cap,
-                            stream=st.cuda_stream, check=False)
-                if timed:
-                    e2.record(st)
-                    ev.append((e0, e1, e2))
+                    if timed:
+                        e1.record(st)
+                    plan.decode_ctx(ids[a:b], cx, P, cnt, ent, cap,
+                                    stream=st.cuda_stream)
+                    plan.decode(cx, ids[a:b], coded[a:b], dec[a:b],
+                                data=data[a:b], counts=cnt, entries=ent,
+                                cap=cap, stream=st.cuda_stream, check=False)
+                    if timed:
+                        e2.record(st)
+                        ev.append((e0, e1, e2))
+
+        def check():
+            # every stripe decoded back to its data, no OOR bucket overflowed
+            # (a count above cap would also raise the plan's sticky error)
+            return (bool(torch.equal(dec, data)) and plan.take_error() == 0
+                    and int(counts.max().item()) <= cap)
+
+    def sync():
+        if not dry:
+            torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step(False)
-    torch.cuda.synchronize()
-    # correctness of the measured pipeline (outside the timed region)
-    ok = bool(torch.equal(dec, data)) and plan.take_error() == 0
-    oor_max = int(counts.max().item())
+    sync()
+    ok = check()  # the measured pipeline, outside the timed region
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ok = ok and plan.take_error() == 0
+    # and again after the timed steps (their last decode), outside the timer
+    ok = ok and check()
     if dist:
         elapsed, ok = reduce_over_ranks(dist, elapsed, ok, dev)
 
     enc_b, dec_b = alg_bytes(k, m, P, sys_)
     value = aggregate_value(world, S, args.steps, k, m, P, elapsed, sys_)
-    enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
-    dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
-    # per launch: C stripes (the whole batch unless chunked)
-    enc_gbs = C * enc_b / (enc_ms * 1e-3) / 1e9
-    dec_gbs = C * dec_b / (dec_ms * 1e-3) / 1e9
+    enc_ms = dec_ms = enc_gbs = dec_gbs = None  # dry run: no kernels
+    if ev:
+        enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+        dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+        # per launch: C stripes (the whole batch unless chunked)
+        enc_gbs = C * enc_b / (enc_ms * 1e-3) / 1e9
+        dec_gbs = C * dec_b / (dec_ms * 1e-3) / 1e9
 
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -232,13 +385,11 @@ def main():
     K = 1
     while K < k:
         K *= 2
-    name = (f"RS-FNT{'-sys' if sys_ else ''} k={k} n={plan.n} "
+    name = (f"RS-FNT{'-sys' if sys_ else ''} k={k} n={n} "
             f"pkt={pkt_bytes // 1024}KiB")
     metric = ("device-resident encode+decode GB/s per GPU, RS-FNT k=16 n=64 "
               "pkt=64KiB" if headline else
               f"device-resident encode+decode GB/s per GPU, {name}")
-    # the matrix path runs on the matrix cores for k <= 64
-    # (matrix_pack.h MatLayout::KS), on the dot2 kernel otherwise
     mat_kernel = "matrix_mfma_kernel<*>" if k <= 64 else "matrix_kernel<*>"
     enc_kernel = (f"encode_fnt_kernel<{K},*>" if not sys_ and K <= 64
                   else mat_kernel)
@@ -257,7 +408,7 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"{name} encode+decode, batch={S} stripes per GPU",
-            "k": k, "m": m, "n": plan.n, "pkt_bytes": pkt_bytes,
+            "k": k, "m": m, "n": n, "pkt_bytes": pkt_bytes,
             "systematic": sys_,
             "stripes_per_gpu": S,
             "decode": "per-stripe random n-k erasures, contexts built "
@@ -272,23 +423,23 @@ def main():
         "decode_ms": dec_ms,
         "decode_GBps": dec_gbs,
         "roundtrip_ok": ok,
-        "oor_max_per_bucket": oor_max,
         "roofline": {
             "bound": "hbm",
             "kernel": enc_kernel,
             "achieved": enc_gbs,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": enc_gbs / HBM_PEAK_GBS,
+            "frac": enc_gbs / HBM_PEAK_GBS if enc_gbs else None,
             "traffic": traffic,
             "bytes_per_launch": C * enc_b,
         },
         "cpu_baseline": None,
+        "build_id": None if dry else qa.build_id(),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        out["cpu_baseline"] = cpu_baseline(k, m, P, threads, args.cpu_stripes,
-                                           sys_)
+    if dry:
+        out["dry_run"] = True
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not dry:
+        out["cpu_baseline"] = cpu_baseline(k, m, P, sys_, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

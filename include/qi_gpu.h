@@ -23,8 +23,9 @@
  * OOR marks are kept in *buckets*: counts[s*slots + slot] (u32) and
  * entries[(s*slots + slot)*cap + e] (u32 word offset within the row).  Encode
  * zeroes nothing: callers clear counts (qi_gpu_oor_clear) before encoding.
- * Entries inside a bucket are unordered; counts may exceed cap (overflow,
- * detected by the caller).
+ * Entries inside a bucket are unordered; encode keeps counting past cap (the
+ * caller detects the overflow from the count and re-runs with a larger
+ * cap); a decode reading such a bucket raises qi_gpu_take_error.
  */
 #ifndef QI_GPU_H
 #define QI_GPU_H
@@ -113,9 +114,15 @@ int qi_gpu_decode_packed(qi_plan* plan, const void* d_ctx,
                          long long out_row_stride, long long words,
                          int n_stripes, void* stream);
 
-/* Non-zero if a decode overflowed its per-tile OOR scratch (sticky; reset
- * by reading). Synchronous. */
+/* Non-zero if an OOR bucket read by a decode context or a decode held more
+ * marks than its capacity (oor_cap), i.e. some out-of-range symbols could
+ * not be restored and the affected stripes are wrong (sticky per plan; reset
+ * by reading).  Synchronous.  Tiles with many marks need no capacity of
+ * their own: they are decoded by a slower path, never refused. */
 int qi_gpu_take_error(qi_plan* plan);
+
+/* Build identification: "<git describe>+src:<hash of the library sources>". */
+const char* qi_build_id(void);
 
 
 /* ---- Block API over host buffers (C view of qi::fec::RsFnt, see

@@ -14,6 +14,7 @@
  * Properties::fnt_serialize / fnt_deserialize.
  */
 #include <chrono>
+#include <memory>
 #include <cstdint>
 #include <cstring>
 #include <thread>
@@ -415,20 +416,24 @@ int ref_nf4_decode_blocks(int ws, int k, int m, size_t pkt, uint8_t** data,
 
 /*
  * CPU baseline: `threads` independent replicas (the reference bench's -g
- * model, benchmark/benchmark.cpp:813-817), each encoding `stripes` stripes
- * of k fragments x pkt words (one encode_blocks_vertical call per stripe,
- * pkt_size = pkt), then decoding each from a fixed erasure pattern (the
- * first k of the last fragments... see `pattern`).  Returns wall seconds
- * for the whole job; enc_s/dec_s receive the per-phase sums of thread 0.
+ * model, benchmark/benchmark.cpp:813-817), each repeatedly encoding one
+ * stripe of k fragments x pkt words (one encode_blocks_vertical call,
+ * pkt_size = pkt) and decoding it back from a fixed erasure pattern
+ * (`missing`), until `min_seconds` of wall time have passed (at least one
+ * stripe each).  Returns the wall seconds of the whole job; *stripes
+ * receives the stripes done by all threads together, enc_s/dec_s the
+ * per-phase sums of thread 0.
  */
-double ref_bench(int sys, int k, int m, size_t pkt, int stripes, int threads,
-                 const int* missing, double* enc_s, double* dec_s)
+double ref_bench(int sys, int k, int m, size_t pkt, double min_seconds, int threads,
+                 const int* missing, long long* stripes, double* enc_s,
+                 double* dec_s)
 {
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> pool;
     std::vector<double> te(threads, 0), td(threads, 0);
+    std::vector<long long> done(threads, 0);
     for (int t = 0; t < threads; t++) {
-        pool.emplace_back([=, &te, &td]() {
+        pool.emplace_back([=, &te, &td, &done]() {
             std::unique_ptr<RsFnt<uint32_t>> f(make(sys, k, m, pkt));
             unsigned no = f->n_outputs;
             size_t bytes = pkt * 2;
@@ -455,7 +460,7 @@ double ref_bench(int sys, int k, int m, size_t pkt, int stripes, int threads,
                 unsigned id = sys ? k + i : i;
                 pv[i] = miss[id] ? nullptr : ov[i];
             }
-            for (int it = 0; it < stripes; it++) {
+            for (;;) {
                 auto a = std::chrono::steady_clock::now();
                 f->encode_blocks_vertical(dv, ov, props, wanted, bytes);
                 auto b = std::chrono::steady_clock::now();
@@ -466,12 +471,20 @@ double ref_bench(int sys, int k, int m, size_t pkt, int stripes, int threads,
                 auto c = std::chrono::steady_clock::now();
                 te[t] += std::chrono::duration<double>(b - a).count();
                 td[t] += std::chrono::duration<double>(c - b).count();
+                done[t]++;
+                if (std::chrono::duration<double>(c - t0).count() >= min_seconds)
+                    break;
             }
         });
     }
     for (auto& th : pool)
         th.join();
     auto t1 = std::chrono::steady_clock::now();
+    long long total = 0;
+    for (long long v : done)
+        total += v;
+    if (stripes)
+        *stripes = total;
     if (enc_s)
         *enc_s = te[0];
     if (dec_s)

@@ -55,6 +55,7 @@ def _declare(lib):
         "qi_gpu_decode_packed": (I, [V, V, V, LL, LL, V, V, I, V, LL, LL, LL,
                                      I, V]),
         "qi_gpu_take_error": (I, [V]),
+        "qi_build_id": (C.c_char_p, []),
         "qi_fec_new": (V, [I, I, I]),
         "qi_fec_delete": (None, [V]),
         "qi_fec_n_outputs": (I, [V]),
@@ -96,6 +97,48 @@ def lib():
             pass
         _lib = _declare(C.CDLL(LIB_PATH))
     return _lib
+
+
+def build_id():
+    """'<git describe>+src:<source hash>' baked into the loaded library."""
+    return lib().qi_build_id().decode()
+
+
+def _rows(t, name, rows=None, stripes=None):
+    """Check a [S, rows, P] u16 row tensor before its pointer and strides go
+    to the device C-ABI: a wrong dtype, device, shape or a non-unit inner
+    stride would become out-of-bounds device accesses."""
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name}: expected a HIP (cuda) tensor")
+    if t.dtype not in (torch.int16, torch.uint16):
+        raise TypeError(f"{name}: expected int16/uint16, got {t.dtype}")
+    if t.dim() != 3 or t.stride(-1) != 1:
+        raise ValueError(f"{name}: expected [S, rows, P] with unit inner stride")
+    if rows is not None and t.shape[1] != rows:
+        raise ValueError(f"{name}: expected {rows} rows, got {t.shape[1]}")
+    if stripes is not None and t.shape[0] != stripes:
+        raise ValueError(f"{name}: expected {stripes} stripes, got {t.shape[0]}")
+
+
+def _flat(t, name, n, dtypes):
+    """A device buffer of at least n elements of one of `dtypes`."""
+    if t is None:
+        return
+    if not t.is_cuda or t.dtype not in dtypes or not t.is_contiguous():
+        raise TypeError(f"{name}: expected a contiguous HIP tensor of {dtypes}")
+    if t.numel() < n:
+        raise ValueError(f"{name}: {t.numel()} elements, need {n}")
+
+
+def _oor(counts, entries, cap, S, slots):
+    import torch
+    if counts is None:
+        return
+    if entries is None or cap < 1:
+        raise ValueError("OOR buckets need counts, entries and cap >= 1")
+    _flat(counts, "counts", S * slots, (torch.int32,))
+    _flat(entries, "entries", S * slots * cap, (torch.int32,))
 
 
 def require_device():
@@ -142,8 +185,12 @@ class Plan:
 
     def encode(self, data, out, counts=None, entries=None, cap=0, stream=None):
         """data: int16/uint16 tensor [S, k, P] on cuda; out: [S, n_out, P]."""
+        _rows(data, "data", self.k)
         S, k, P = data.shape
-        assert k == self.k and out.shape[1] == self.n_outputs
+        _rows(out, "out", self.n_outputs, S)
+        if out.shape[2] < P:
+            raise ValueError("out: fewer columns than data")
+        _oor(counts, entries, cap, S, self.n_outputs)
         rc = lib().qi_gpu_encode(
             self.h, data.data_ptr(), data.stride(0), data.stride(1),
             out.data_ptr(), out.stride(0), out.stride(1), P, S,
@@ -160,6 +207,11 @@ class Plan:
                    h_ids=None, stream=None):
         """ids: int16 tensor [S, k] on cuda (fragment ids); OOR buckets of
         the coded rows as produced by encode (routed into the contexts)."""
+        import torch
+        S = ids.shape[0]
+        _flat(ids, "ids", S * self.k, (torch.int16, torch.uint16))
+        _flat(ctx, "ctx", self.ctx_bytes(S, words), (torch.uint8,))
+        _oor(counts, entries, cap, S, self.n_outputs)
         rc = lib().qi_gpu_decode_ctx(
             self.h, ids.data_ptr(),
             h_ids.ctypes.data_as(C.c_void_p) if h_ids is not None else None,
@@ -176,7 +228,15 @@ class Plan:
         check: synchronise and return the sticky OOR-overflow flag
         (qi_gpu_take_error); with check=False the call stays asynchronous
         and returns 0 -- call take_error() later."""
+        import torch
+        _rows(out, "out", self.k)
         S, _, P = out.shape
+        _rows(coded, "coded", self.n_outputs, S)
+        if data is not None:
+            _rows(data, "data", self.k, S)
+        _flat(ids, "ids", S * self.k, (torch.int16, torch.uint16))
+        _flat(ctx, "ctx", self.ctx_bytes(S, P), (torch.uint8,))
+        _oor(counts, entries, cap, S, self.n_outputs)
         d = data if data is not None else coded
         rc = lib().qi_gpu_decode(
             self.h, ctx.data_ptr(), ids.data_ptr(), d.data_ptr(), d.stride(0),
@@ -193,6 +253,11 @@ class Plan:
                           cap=0, h_ids=None, stream=None):
         """Contexts for decode_packed: OOR buckets indexed by the position
         of the received row (slots = k)."""
+        import torch
+        S = ids.shape[0]
+        _flat(ids, "ids", S * self.k, (torch.int16, torch.uint16))
+        _flat(ctx, "ctx", self.ctx_bytes(S, words), (torch.uint8,))
+        _oor(counts, entries, cap, S, self.k)
         rc = lib().qi_gpu_decode_ctx_packed(
             self.h, ids.data_ptr(),
             h_ids.ctypes.data_as(C.c_void_p) if h_ids is not None else None,
@@ -206,7 +271,12 @@ class Plan:
     def decode_packed(self, ctx, recv, out, counts=None, entries=None, cap=0,
                       stream=None, check=True):
         """recv: [S, k, P] received rows in id order; out: [S, k, P]."""
+        import torch
+        _rows(out, "out", self.k)
         S, _, P = out.shape
+        _rows(recv, "recv", self.k, S)
+        _flat(ctx, "ctx", self.ctx_bytes(S, P), (torch.uint8,))
+        _oor(counts, entries, cap, S, self.k)
         rc = lib().qi_gpu_decode_packed(
             self.h, ctx.data_ptr(), recv.data_ptr(), recv.stride(0),
             recv.stride(1),

@@ -143,8 +143,14 @@ RsFnt::RsFnt(FecType t, unsigned ws, unsigned k, unsigned m, size_t pkt)
         throw std::runtime_error(
             "RsFnt: cannot create the GPU plan (no HIP device or k > 128)");
     n = static_cast<unsigned>(qi_plan_n(plan_));
-    check(hipStreamCreateWithFlags(&plan_->host.stream, hipStreamNonBlocking),
-          "hipStreamCreate");
+    const hipError_t e =
+        hipStreamCreateWithFlags(&plan_->host.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        // the destructor does not run for a throwing constructor
+        qi_plan_destroy(plan_);
+        plan_ = nullptr;
+        check(e, "hipStreamCreate");
+    }
 }
 
 RsFnt::~RsFnt()
@@ -296,7 +302,7 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
                   "D2H");
     check(hipStreamSynchronize(s), "sync");
     if (qi_gpu_take_error(plan_))
-        throw std::runtime_error("RsFnt: too many OOR marks in one tile");
+        throw std::runtime_error("RsFnt: OOR marks lost (bucket capacity)");
 }
 
 void RsFnt::encode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
@@ -662,7 +668,7 @@ bool RsFnt::decode_streams_vertical(
         check(hipStreamSynchronize(sl.st), "sync");
         sl.busy = false;
         if (qi_gpu_take_error(plan_))
-            throw std::runtime_error("RsFnt: too many OOR marks in one tile");
+            throw std::runtime_error("RsFnt: OOR marks lost (bucket capacity)");
         const uint8_t* hout = sl.host + io_b;
         parallel_for(k, [&](size_t i) {
             if (output_data_bufs[i])

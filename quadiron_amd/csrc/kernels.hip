@@ -14,6 +14,8 @@
 // BUF=false instantiation (flat global addressing).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "fnt_codelets.h"
 #include "gf65537.h"
 #include "matrix_pack.h"
@@ -81,19 +83,12 @@ struct Region {
 // written through the XCD's L2) +5 % on both the encode shape (16 rows in,
 // 64 out) and the decode shape (16 of 64 rows in, 16 out); nt loads +5 % on
 // the decode shape, but slow the encode shape down (its inputs stay plain).
-#ifndef QI_AUX_LD
-#define QI_AUX_LD 2
-#endif
-#ifndef QI_AUX_ST
-#define QI_AUX_ST 18
-#endif
-constexpr int kAuxLd = QI_AUX_LD;
-constexpr int kAuxSt = QI_AUX_ST;
-// cache policy of the matrix-core kernel's whole-line output stores
-#ifndef QI_AUX_ST_MF
-#define QI_AUX_ST_MF QI_AUX_ST
-#endif
-constexpr int kAuxStMf = QI_AUX_ST_MF;
+// The matrix-core kernel's whole-line output stores keep nt|sc1 as well:
+// default, nt and sc1 alone measured 1-7 % slower
+// (profiles/r1_ab_mfma_store_policy.txt).
+constexpr int kAuxLd = 2;
+constexpr int kAuxSt = 18;
+constexpr int kAuxStMf = 18;
 
 // XCD-aware block -> (stripe, tile) map.  Workgroups are dispatched
 // round-robin over the 8 XCDs (block b runs on XCD b % 8), so with the plain
@@ -102,38 +97,20 @@ constexpr int kAuxStMf = QI_AUX_ST_MF;
 // walks all tiles of stripe 8g + x: +4-6 % HBM throughput on both kernel
 // shapes (membw3 "ord3").  A trailing partial group (S % 8 stripes) keeps
 // the stripe-major order.
-#ifndef QI_XCD_MAP
-#define QI_XCD_MAP 1
-#endif
 __device__ __forceinline__ void block_map(int b, int tiles, int& s, int& tile)
 {
-    if constexpr (QI_XCD_MAP) {
-        const int n_stripes = static_cast<int>(gridDim.x) / tiles;
-        const int grouped = (n_stripes & ~7) * tiles;  // blocks in full groups
-        if (b < grouped) {
-            const int j = b >> 3;
-            const int g = j / tiles;
-            s = g * 8 + (b & 7);
-            tile = j - g * tiles;
-            return;
-        }
+    const int n_stripes = static_cast<int>(gridDim.x) / tiles;
+    const int grouped = (n_stripes & ~7) * tiles;  // blocks in full groups
+    if (b < grouped) {
+        const int j = b >> 3;
+        const int g = j / tiles;
+        s = g * 8 + (b & 7);
+        tile = j - g * tiles;
+        return;
     }
     s = b / tiles;
     tile = b - s * tiles;
 }
-// K values (bit log2 K) whose encode body re-reads its inputs every pass:
-// K = 32 (141 -> 105 VGPRs, 3 -> 4 waves/SIMD).  K = 64 stays resident (the
-// DFT64 codelet alone needs ~180 VGPRs, so reloading gains no occupancy).
-#ifndef QI_ENC_PAIR
-#define QI_ENC_PAIR 0
-#endif
-// waves per SIMD the K = 64 encode body is compiled for (A/B knob)
-#ifndef QI_ENC_K64_WAVES
-#define QI_ENC_K64_WAVES 2
-#endif
-#ifndef QI_ENC_RELOAD_MASK
-#define QI_ENC_RELOAD_MASK (1 << 5)
-#endif
 
 // NDW (1 or 2) dwords per lane of the row at byte offset `row`
 template <int NDW, bool BUF, int AUX = 0>
@@ -266,46 +243,27 @@ __device__ __forceinline__ void encode_body(
     const Region<BUF>& gi, uint32_t irs, const Region<BUF>& go, uint32_t ors,
     uint32_t voff, long long col, long long avail, int s, const Oor& oor)
 {
-    // RELOAD (large K): re-read the K input rows every pass (L2 hits after
-    // the first) instead of keeping them live next to the pass's outputs --
-    // halves the VGPRs of the K = 32/64 bodies
-    constexpr bool RELOAD = ((QI_ENC_RELOAD_MASK) >> ilog2c(K)) & 1;
-    // PAIRED (full tiles, 2 columns per lane): passes 2w and 2w+1 are stored
-    // together, row 4u+2w then 4u+2w+1, ...  Storing a pass alone writes 16
-    // rows that share the row-index bits below log2(passes) -- the 64 KiB
-    // address bit(s) -- and measures 7 % slower in HBM than storing rows with
-    // that bit alternating (membw3 "ro1" vs "ro2").  The inputs are then kept
-    // as the loaded u16 pairs (K dwords, unpacked at use) to pay for the K
-    // held dwords of the even pass.
-    constexpr bool PAIRED = QI_ENC_PAIR && FULL && COLS == 2 && !RELOAD;
+    // RELOAD (K = 32): re-read the K input rows every pass (L2 hits after
+    // the first) instead of keeping them live next to the pass's outputs:
+    // 141 -> 105 VGPRs, 3 -> 4 waves/SIMD.  K = 64 stays resident (its DFT64
+    // codelet alone needs ~180 VGPRs, so reloading gains no occupancy).
+    // Holding two passes to interleave their stores (the 64 KiB address bit
+    // alternating, +7 % on the bare store pattern) measured 3 % slower on
+    // the real kernel (16 more VGPRs + unpacks), so passes store alone.
+    constexpr bool RELOAD = K == 32;
     const int passes = n / K;
-    const bool paired = PAIRED && (passes & 1) == 0;  // uniform
 
-    uint32_t xw[PAIRED ? K : 1];  // PAIRED: [col1 | col0] per input row
-    int32_t x[PAIRED ? 1 : COLS][K];
+    int32_t x[COLS][K];
     auto load_x = [&](uint32_t vo) {
 #pragma unroll
         for (int t = 0; t < K; t++) {
             const int row = KEQ ? t : (t < k ? t : k - 1);  // clamp, then mask
-            if constexpr (PAIRED) {
-                uint32_t w[1];
-                ld_dw<1, BUF>(gi, static_cast<uint32_t>(row) * irs, vo, w);
-                xw[t] = (KEQ || t < k) ? w[0] : 0u;
-            } else {
-                int32_t v[COLS];
-                ld<COLS, FULL, BUF>(gi, static_cast<uint32_t>(row) * irs, vo, avail,
-                                    v);
+            int32_t v[COLS];
+            ld<COLS, FULL, BUF>(gi, static_cast<uint32_t>(row) * irs, vo, avail, v);
 #pragma unroll
-                for (int c = 0; c < COLS; c++)
-                    x[c][t] = (KEQ || t < k) ? v[c] : 0;
-            }
+            for (int c = 0; c < COLS; c++)
+                x[c][t] = (KEQ || t < k) ? v[c] : 0;
         }
-    };
-    auto xin = [&](int c, int t) -> int32_t {
-        if constexpr (PAIRED)
-            return static_cast<int32_t>(c == 0 ? xw[t] & 0xffffu : xw[t] >> 16);
-        else
-            return x[c][t];
     };
     if constexpr (!RELOAD)
         load_x(voff);
@@ -317,19 +275,12 @@ __device__ __forceinline__ void encode_body(
             asm volatile("" : "+v"(vo));  // keep the loads inside the loop
             load_x(vo);
         }
-        if constexpr (PAIRED) {
-            // opaque per pass: keeps the unpacking inside the pass (hoisted,
-            // the 2K unpacked inputs would stay live and spill)
-#pragma unroll
-            for (int t = 0; t < K; t++)
-                asm volatile("" : "+v"(xw[t]));
-        }
         if (v == 0) {
 #pragma unroll
             for (int c = 0; c < COLS; c++) {
 #pragma unroll
                 for (int t = 0; t < K; t++)
-                    y[c][t] = xin(c, t);
+                    y[c][t] = x[c][t];
                 dft<K, 0, 65535>(y[c]);
             }
         } else {
@@ -342,7 +293,7 @@ __device__ __forceinline__ void encode_body(
                 const int32_t cb = tw[t];
 #pragma unroll
                 for (int c = 0; c < COLS; c++)
-                    y[c][t] = t == 0 ? xin(c, t) : fold(mul_i24_s(xin(c, t), cb));
+                    y[c][t] = t == 0 ? x[c][t] : fold(mul_i24_s(x[c][t], cb));
             }
 #pragma unroll
             for (int c = 0; c < COLS; c++)
@@ -386,70 +337,36 @@ __device__ __forceinline__ void encode_body(
     // CHK: some rows >= n_out are not wanted (uniform per launch; the
     // checks become a scalar branch around every store, so the common
     // all-rows case gets its own branch-free copy)
-    auto store_row = [&](auto chk, int row, const int32_t (&y)[COLS][K], int u) {
-        uint32_t o[COLS];
-#pragma unroll
-        for (int c = 0; c < COLS; c++)
-            o[c] = static_cast<uint32_t>(y[c][u]);
-        if (!decltype(chk)::value || row < n_out)
-            st<COLS, FULL, BUF, kAuxSt>(go, static_cast<uint32_t>(row) * ors, voff,
-                                        avail, o);
-    };
-    auto run_paired = [&](auto chk) {
-        for (int v = 0; v < passes; v += 2) {
-            int32_t y[COLS][K];
-            compute(v, y);
-            fixup(v, y);
-            uint32_t held[K];
-#pragma unroll
-            for (int u = 0; u < K; u++)
-                held[u] = pack_lo(static_cast<uint32_t>(y[0][u]),
-                                  static_cast<uint32_t>(y[1][u]));
-            compute(v + 1, y);
-            fixup(v + 1, y);
-#pragma unroll
-            for (int u = 0; u < K; u++) {
-                const int row = passes * u + v;
-                if (!decltype(chk)::value || row < n_out) {
-                    const uint32_t w[1] = {held[u]};
-                    st_dw<1, BUF, kAuxSt>(go, static_cast<uint32_t>(row) * ors, voff,
-                                          w);
-                }
-                store_row(chk, row + 1, y, u);
-            }
-        }
-    };
     auto run = [&](auto chk) {
         for (int v = 0; v < passes; v++) {
             int32_t y[COLS][K];
             compute(v, y);
             fixup(v, y);
 #pragma unroll
-            for (int u = 0; u < K; u++)
-                store_row(chk, passes * u + v, y, u);
+            for (int u = 0; u < K; u++) {
+                const int row = passes * u + v;
+                uint32_t o[COLS];
+#pragma unroll
+                for (int c = 0; c < COLS; c++)
+                    o[c] = static_cast<uint32_t>(y[c][u]);
+                if (!decltype(chk)::value || row < n_out)
+                    st<COLS, FULL, BUF, kAuxSt>(go, static_cast<uint32_t>(row) * ors,
+                                                voff, avail, o);
+            }
         }
     };
-    using all_rows = std::integral_constant<bool, false>;
-    using some_rows = std::integral_constant<bool, true>;
-    if constexpr (PAIRED) {
-        if (paired) {
-            if (n_out >= n)
-                run_paired(all_rows{});
-            else
-                run_paired(some_rows{});
-            return;
-        }
-    }
     if (n_out >= n)
-        run(all_rows{});
+        run(std::integral_constant<bool, false>{});
     else
-        run(some_rows{});
+        run(std::integral_constant<bool, true>{});
 }
 
 template <int K, int COLS, bool KEQ, bool BUF>
 // 4 waves per SIMD: the K=16, COLS=2 body fits 128 VGPRs without spills or
-// extra instructions (3 waves at the compiler's default 130)
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 64 ? QI_ENC_K64_WAVES : 4))) void
+// extra instructions (3 waves at the compiler's default 130).  K = 64: 2
+// waves (3 waves = 168 VGPRs spilled and ran 20 % slower,
+// profiles/r1_ab_k64_encode.txt)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 64 ? 2 : 4))) void
 encode_fnt_kernel(
     int k, int n, int n_out, const int32_t* __restrict__ twist,
     const uint16_t* __restrict__ data, long long dss, uint32_t irs,
@@ -492,6 +409,80 @@ struct MatExt {
     uint32_t e0, e1, eo;
     long long c0;
 };
+
+// Where the OOR marks of the received rows (decode_prepare's restore of
+// 65536, src/fec_base.h:1361-1404) come from in a matrix launch.  A tile
+// normally takes them from the context's route table or from one scan of
+// the buckets into LDS (kMaxTileOor entries); a tile holding more marks
+// than that (adversarial data) sets `slow` and every epilogue walks the
+// buckets directly -- slower, but with no limit, as the reference has none.
+struct OorScan {
+    Oor in;
+    const int32_t* sid;  // per-stripe ids (nullptr = identity)
+    int by_pos, slot_base, kin, s;
+    bool slow;
+};
+
+// f(position, word offset) for every mark of the received rows; a bucket
+// whose count exceeds its capacity lost entries on the way in: sticky
+// error kErrOorTruncated (the result of that stripe is not trustworthy)
+template <typename F>
+__device__ __forceinline__ void for_each_bucket_mark(const OorScan& sc, uint32_t* err,
+                                                     F f)
+{
+    for (int i = 0; i < sc.kin; i++) {
+        const int id = sc.sid ? sc.sid[i] : i;
+        const int slot = (sc.by_pos ? i : id) - sc.slot_base;
+        if (slot < 0)
+            continue;
+        const long long bk = static_cast<long long>(sc.s) * sc.in.slots + slot;
+        uint32_t c = sc.in.counts[bk];
+        if (c > static_cast<uint32_t>(sc.in.cap)) {
+            if (err)
+                atomicOr(err, kErrOorTruncated);
+            c = static_cast<uint32_t>(sc.in.cap);
+        }
+        for (uint32_t e = 0; e < c; e++)
+            f(i, sc.in.entries[bk * sc.in.cap + e]);
+    }
+}
+
+// block-wide scan of the buckets into the LDS list (s_i, s_col) of the
+// marks inside columns [col0, col1); returns the number of marks found
+// (> kMaxTileOor: the list is incomplete, use the slow path)
+__device__ __forceinline__ int scan_tile_marks(const OorScan& sc, long long col0,
+                                               long long col1, long long words,
+                                               int* s_cnt, int* s_i, uint32_t* s_col,
+                                               uint32_t* err)
+{
+    if (threadIdx.x == 0)
+        *s_cnt = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < sc.kin; i += blockDim.x) {
+        const int id = sc.sid ? sc.sid[i] : i;
+        const int slot = (sc.by_pos ? i : id) - sc.slot_base;
+        if (slot < 0)
+            continue;
+        const long long bk = static_cast<long long>(sc.s) * sc.in.slots + slot;
+        uint32_t c = sc.in.counts[bk];
+        if (c > static_cast<uint32_t>(sc.in.cap)) {
+            atomicOr(err, kErrOorTruncated);
+            c = static_cast<uint32_t>(sc.in.cap);
+        }
+        for (uint32_t e = 0; e < c; e++) {
+            const uint32_t w = sc.in.entries[bk * sc.in.cap + e];
+            if (w >= col0 && w < col1 && w < words) {
+                const int p = atomicAdd(s_cnt, 1);
+                if (p < kMaxTileOor) {
+                    s_i[p] = i;
+                    s_col[p] = w;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    return *s_cnt;
+}
 
 template <int KP, int COLS, bool FULL, bool BUF>
 __device__ __forceinline__ void matrix_load(const int (&idv)[2 * KP],
@@ -552,7 +543,7 @@ __device__ __forceinline__ void matrix_compute(
     const int32_t (&xp)[COLS][KP], const Region<BUF>& go, uint32_t ors,
     uint32_t voff, long long col, long long col0, long long avail, int s,
     int n_rm, const uint32_t* rm, int n_lm, const int* s_i,
-    const uint32_t* s_col, const Oor& out_oor)
+    const uint32_t* s_col, const OorScan& sc, uint32_t* err, const Oor& out_oor)
 {
     // M: the per-stripe matrix block (wave-uniform: scalar loads)
     const int kin = L.kin;
@@ -581,17 +572,7 @@ __device__ __forceinline__ void matrix_compute(
         for (int c = 0; c < COLS; c++)
             y[c] = fold(acc[c]);  // T-range
         // restored OOR symbols: 65536 == -1 where the stored word is 0
-        for (int e = 0; e < n_rm + n_lm; e++) {
-            long long w;
-            int pos;
-            if (e < n_rm) {
-                const uint32_t v = rm[e];
-                pos = static_cast<int>(v >> 16);
-                w = rbase + (v & 0xffffu);
-            } else {
-                pos = s_i[e - n_rm];
-                w = s_col[e - n_rm];
-            }
+        auto restore = [&](int pos, long long w) {
             const long long d = w - col;
             if (d >= 0 && d < COLS) {
                 const int32_t corr = plain[t * kin + pos];
@@ -599,6 +580,19 @@ __device__ __forceinline__ void matrix_compute(
                 for (int c = 0; c < COLS; c++)
                     if (c == d)
                         y[c] = fold(fold(y[c] - corr));
+            }
+        };
+        if (sc.slow) {  // block-uniform, rare
+            for_each_bucket_mark(sc, nullptr,
+                                 [&](int pos, uint32_t w) { restore(pos, w); });
+        } else {
+            for (int e = 0; e < n_rm + n_lm; e++) {
+                if (e < n_rm) {
+                    const uint32_t v = rm[e];
+                    restore(static_cast<int>(v >> 16), rbase + (v & 0xffffu));
+                } else {
+                    restore(s_i[e - n_rm], s_col[e - n_rm]);
+                }
             }
         }
         const int32_t rs = rscale[t];
@@ -700,45 +694,22 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
         matrix_load<KP, COLS, false, BUF>(idv, src, g0, g1, voff,
                                           words - col, xp);
     }
+    OorScan sc{in_oor, sid, src.by_pos, slot_base, kin, s, false};
     int n_lm = 0;
     if (scan) {  // block-uniform
-        if (threadIdx.x == 0)
-            s_cnt = 0;
-        __syncthreads();
-        for (int i = threadIdx.x; i < kin; i += kBlock) {
-            const int id = sid ? sid[i] : i;
-            const int slot = (src.by_pos ? i : id) - slot_base;
-            if (slot < 0)
-                continue;
-            const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
-            uint32_t c = in_oor.counts[bk];
-            if (c > static_cast<uint32_t>(in_oor.cap))
-                c = in_oor.cap;
-            for (uint32_t e = 0; e < c; e++) {
-                const uint32_t w = in_oor.entries[bk * in_oor.cap + e];
-                if (w >= col0 && w < col1 && w < words) {
-                    const int p = atomicAdd(&s_cnt, 1);
-                    if (p < kMaxTileOor) {
-                        s_i[p] = i;
-                        s_col[p] = w;
-                    } else {
-                        atomicOr(err, 1u);
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        n_lm = min(s_cnt, kMaxTileOor);
+        const int cnt = scan_tile_marks(sc, col0, col1, words, &s_cnt, s_i, s_col, err);
+        sc.slow = cnt > kMaxTileOor;
+        n_lm = sc.slow ? 0 : cnt;
     }
     const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
     if (full) {
         matrix_compute<KP, COLS, true, BUF>(L, M, xp, go, ors, voff, col, col0,
                                             COLS, s, n_rm, rm, n_lm, s_i, s_col,
-                                            out_oor);
+                                            sc, err, out_oor);
     } else if (col < words) {
         matrix_compute<KP, COLS, false, BUF>(L, M, xp, go, ors, voff, col, col0,
                                              words - col, s, n_rm, rm, n_lm, s_i,
-                                             s_col, out_oor);
+                                             s_col, sc, err, out_oor);
     }
 }
 
@@ -917,37 +888,15 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                 static_cast<uint16_t>(lo);
         }
     }
+    OorScan sc{in_oor, sid, src.by_pos, slot_base, kin, s, false};
     int n_lm = 0;
-    if (scan) {  // block-uniform
-        if (threadIdx.x == 0)
-            *s_cnt = 0;
+    if (scan) {  // block-uniform; the scan's barriers also publish the image
+        const int cnt = scan_tile_marks(sc, col0, col1, words, s_cnt, s_i, s_col, err);
+        sc.slow = cnt > kMaxTileOor;
+        n_lm = sc.slow ? 0 : cnt;
+    } else {
         __syncthreads();
-        for (int i = threadIdx.x; i < kin; i += kBlock) {
-            const int id = sid ? sid[i] : i;
-            const int slot = (src.by_pos ? i : id) - slot_base;
-            if (slot < 0)
-                continue;
-            const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
-            uint32_t c = in_oor.counts[bk];
-            if (c > static_cast<uint32_t>(in_oor.cap))
-                c = in_oor.cap;
-            for (uint32_t e = 0; e < c; e++) {
-                const uint32_t wc = in_oor.entries[bk * in_oor.cap + e];
-                if (wc >= col0 && wc < col1 && wc < words) {
-                    const int p = atomicAdd(s_cnt, 1);
-                    if (p < kMaxTileOor) {
-                        s_i[p] = i;
-                        s_col[p] = wc;
-                    } else {
-                        atomicOr(err, 1u);
-                    }
-                }
-            }
-        }
     }
-    __syncthreads();
-    if (scan)
-        n_lm = min(*s_cnt, kMaxTileOor);
 
     // matrix cores: wave wv covers COLS super tiles of 64 columns, for each
     // block of 16 output rows in turn (the next block's operands prefetched)
@@ -1024,17 +973,7 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                                              acc[T][0][j]));
             // restored OOR symbols of the received rows: 65536 == -1 where
             // the stored word is 0 (decode_prepare, src/fec_base.h:1361-1404)
-            for (int e = 0; e < n_rm + n_lm; e++) {
-                long long wc;
-                int pos;
-                if (e < n_rm) {
-                    const uint32_t v = rm[e];
-                    pos = static_cast<int>(v >> 16);
-                    wc = rbase + (v & 0xffffu);
-                } else {
-                    pos = s_i[e - n_rm];
-                    wc = s_col[e - n_rm];
-                }
+            auto restore = [&](int pos, long long wc) {
                 const long long d = wc - cb;
                 if (trow && d >= 0 && d < 16) {
                     const int32_t corr = plain[t * kin + pos];
@@ -1042,6 +981,19 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                     for (int c = 0; c < 16; c++)
                         if (c == d)
                             y[c] = fold(fold(y[c] - corr));
+                }
+            };
+            if (sc.slow) {  // block-uniform, rare
+                for_each_bucket_mark(sc, nullptr,
+                                     [&](int pos, uint32_t wc) { restore(pos, wc); });
+            } else {
+                for (int e = 0; e < n_rm + n_lm; e++) {
+                    if (e < n_rm) {
+                        const uint32_t v = rm[e];
+                        restore(static_cast<int>(v >> 16), rbase + (v & 0xffffu));
+                    } else {
+                        restore(s_i[e - n_rm], s_col[e - n_rm]);
+                    }
                 }
             }
             if (__builtin_amdgcn_ballot_w64(rs != 1)) {
@@ -1231,14 +1183,11 @@ __device__ void pack_row_g4(uint32_t* row, const MatLayout& L, int t,
     }
 }
 
-#ifndef QI_CTX_SKIP
-#define QI_CTX_SKIP 0  // timing probe only: skip context phases (wrong results)
-#endif
 template <int NT>
 __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
     int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
-    int by_pos, long long words)
+    int by_pos, long long words, uint32_t* err)
 {
     __shared__ uint32_t xs[64];
     __shared__ uint32_t A[65];
@@ -1272,8 +1221,10 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         if (slot >= 0) {
             const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
             uint32_t c = in_oor.counts[bk];
-            if (c > static_cast<uint32_t>(in_oor.cap))
-                c = in_oor.cap;
+            if (c > static_cast<uint32_t>(in_oor.cap)) {
+                atomicOr(err, kErrOorTruncated);
+                c = static_cast<uint32_t>(in_oor.cap);
+            }
             for (uint32_t e = 0; e < c; e++) {
                 const uint32_t w = in_oor.entries[bk * in_oor.cap + e];
                 if (w >= words)
@@ -1304,11 +1255,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         // 1 / A'(x_i) = 1 / prod_{j != i} (x_i - x_j)
         const uint32_t xi = xs[tid];
         uint32_t den = 1;
-#if !(QI_CTX_SKIP & 4)
         for (int j = 0; j < k; j++)
             if (j != tid)
                 den = mulm(den, subm(xi, xs[j]));
-#endif
         const uint32_t inv = powm(den, 65535u);
         // Q_i = A / (x - x_i) by synthetic division from the top
         uint32_t q = 1;  // A[k]
@@ -1334,7 +1283,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     __syncthreads();
     // 4 lanes per row: pack_row's work split over the row's entries, its
     // reductions over the 4 lanes (k = 64: 92 -> 62 us per 1024 stripes)
-    for (int t = tid / 4; t < ((QI_CTX_SKIP & 1) ? 0 : L.R); t += NT / 4)
+    for (int t = tid / 4; t < L.R; t += NT / 4)
         pack_row_g4(Mt + t * k, L, t, mat, tid & 3);
     if (L.KS()) {
         // the matrix-core operand tiles, from the row-scaled entries in LDS
@@ -1345,7 +1294,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         // zeros included; rows t >= R are zero)
         const int KS = L.KS(), KH = 16 * KS, RBp = L.RB() * 16;
         int32_t* mf = mat + L.mf();
-        for (int it = tid; it < ((QI_CTX_SKIP & 2) ? 0 : RBp * (KH / 4)); it += NT) {
+        for (int it = tid; it < RBp * (KH / 4); it += NT) {
             const int t = it / (KH / 4), i0 = 4 * (it % (KH / 4));
             uint32_t aw = 0, bw = 0;
             if (t < L.R) {
@@ -1541,19 +1490,12 @@ static int mat_dispatch(int cols, const MatLayout& L, const int32_t* mat,
                                    io, slot_base, oo, route, rstride, err, st);
 }
 
-#ifndef QI_MFMA
-#define QI_MFMA 1
-#endif
-// columns per thread of the KS = 1 matrix-core kernel (4: 1024-column
-// blocks, 35 KB LDS; 2: 512-column blocks, 19 KB LDS, more blocks per CU)
-// columns per lane of the KS = 4 (k > 32) kernel: 2 (512-column blocks,
-// 77 KB LDS, 2 blocks/CU) or 1 (256 columns, 44 KB, 3 blocks/CU)
-#ifndef QI_MFMA_COLS4
-#define QI_MFMA_COLS4 2
-#endif
-#ifndef QI_MFMA_COLS1
-#define QI_MFMA_COLS1 4
-#endif
+// columns per lane of the matrix-core kernel: KS = 1 (k <= 16) 4, i.e.
+// 1024-column blocks, 35 KB LDS; KS = 2, 4: 2 (512 columns; at KS = 4 77 KB
+// LDS, 2 blocks/CU).  One u16 column per lane at KS = 4 (256 columns, 44 KB,
+// 3 blocks/CU) slowed the cfg3 decode 0.196 -> 0.205 ms
+// (profiles/r1_ab_mfma_cols1.txt).
+constexpr int kMfmaCols1 = 4, kMfmaCols4 = 2;
 
 template <int KS, int COLS>
 static int mfma_launch(const MatLayout& L, const int32_t* mat, long long ms,
@@ -1567,14 +1509,22 @@ static int mfma_launch(const MatLayout& L, const int32_t* mat, long long ms,
     if (t <= 0 || t * S > 0x7fffffffLL)
         return -1;
     const size_t lds = L.RB() > 1 ? G::kLdsStaged : G::kLds;
-    static bool attr = false;  // dynamic LDS above 64 KiB needs opting in
-    if (G::kLdsStaged > 65536 && !attr) {
-        if (hipFuncSetAttribute(
-                reinterpret_cast<const void*>(&matrix_mfma_kernel<KS, COLS>),
-                hipFuncAttributeMaxDynamicSharedMemorySize,
-                static_cast<int>(G::kLdsStaged)) != hipSuccess)
+    // dynamic LDS above 64 KiB needs opting in, once per device (a bit per
+    // device; a race only repeats the idempotent call)
+    static std::atomic<uint64_t> attr_done{0};
+    if (G::kLdsStaged > 65536) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess)
             return -2;
-        attr = true;
+        const uint64_t bit = dev < 64 ? 1ull << dev : 0;
+        if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
+            if (hipFuncSetAttribute(
+                    reinterpret_cast<const void*>(&matrix_mfma_kernel<KS, COLS>),
+                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                    static_cast<int>(G::kLdsStaged)) != hipSuccess)
+                return -2;
+            attr_done.fetch_or(bit, std::memory_order_release);
+        }
     }
     hipLaunchKernelGGL((matrix_mfma_kernel<KS, COLS>), dim3(t * S), dim3(kBlock),
                        lds, st, L, mat, ms, ids, is, src, dst, ext, words,
@@ -1612,16 +1562,16 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
     // whole kRouteTile column tiles on the matrix cores, the tail (and
     // everything the MFMA kernel does not take) on the dot2 kernel
     const long long wfull = words / kRouteTile * kRouteTile;
-    if (QI_MFMA && L.KS() > 0 && buf && a4 && wfull > 0) {
+    if (L.KS() > 0 && buf && a4 && wfull > 0) {
         int rc;
         if (L.KS() == 1)
-            rc = mfma_launch<1, QI_MFMA_COLS1>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
+            rc = mfma_launch<1, kMfmaCols1>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
                                    S, io, slot_base, oo, route, rstride, err, st);
         else if (L.KS() == 2)
             rc = mfma_launch<2, 2>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
                                    S, io, slot_base, oo, route, rstride, err, st);
         else
-            rc = mfma_launch<4, QI_MFMA_COLS4>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
+            rc = mfma_launch<4, kMfmaCols4>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
                                    S, io, slot_base, oo, route, rstride, err, st);
         if (rc || wfull == words)
             return rc;
@@ -1654,7 +1604,7 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
 int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
                       const uint16_t* d_ids, int S, int32_t* d_ctx,
                       long long ctx_stride, const Oor* in_oor, int slot_base,
-                      int by_pos, long long words, hipStream_t st)
+                      int by_pos, long long words, uint32_t* err, hipStream_t st)
 {
     if (k > 64 || S <= 0)
         return -3;
@@ -1663,11 +1613,11 @@ int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
     if (k > 32)
         hipLaunchKernelGGL(decode_ctx_kernel<256>, dim3(S), dim3(256), lds, st, k, r,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                           slot_base, by_pos, words);
+                           slot_base, by_pos, words, err);
     else
         hipLaunchKernelGGL(decode_ctx_kernel<64>, dim3(S), dim3(64), lds, st, k, r,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                           slot_base, by_pos, words);
+                           slot_base, by_pos, words, err);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

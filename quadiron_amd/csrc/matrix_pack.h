@@ -21,19 +21,16 @@ namespace qi {
 //                  bytes, 3 operand types, 64 lanes x 8 bytes (pack_mf_dword)
 //   kmf[R]         32896 * sum_i c[t][i] mod q (undoes the byte offsets)
 // The MFMA section exists (KS() > 0) when matrix_mfma_kernel takes the
-// block: kin <= 64 (and more than QI_MFMA_MIN_PRODUCTS products per column;
-// 0 = always).  A/B on MI355X, k = 16 decode: 1.54 ms on the matrix cores
-// with the LDS-transposed streaming stores vs 1.62 ms dot2 (1.65 ms before
-// the transpose); the 48 x 16 systematic encode 3.60 vs 3.80 ms and the
-// 64 x 64 decode 0.35 vs 0.62 ms.
-#ifndef QI_MFMA_MIN_PRODUCTS
-#define QI_MFMA_MIN_PRODUCTS 0
-#endif
+// block: kin <= 64.
+// A/B on MI355X, k = 16 decode: 1.54 ms on the matrix cores with the
+// LDS-transposed streaming stores vs 1.62 ms dot2 (1.65 ms before the
+// transpose); the 48 x 16 systematic encode 3.60 vs 3.80 ms and the 64 x 64
+// decode 0.35 vs 0.62 ms.
 struct MatLayout {
     int R, kin, KP;
     QI_HD int KS() const
     {
-        if (kin > 64 || R * kin <= QI_MFMA_MIN_PRODUCTS)
+        if (kin > 64)
             return 0;
         return kin <= 16 ? 1 : kin <= 32 ? 2 : 4;
     }

@@ -52,7 +52,7 @@ int build_ctx(qi_plan* p, const uint16_t* d_ids, const uint16_t* h_ids,
     if (p->k <= 64 && d_ids)
         return launch_decode_ctx(p->k, p->r, mode, L, d_ids, n_stripes,
                                  static_cast<int32_t*>(d_ctx), cs, in, slot_base,
-                                 by_pos, words, s);
+                                 by_pos, words, p->d_err, s);
     if (!h_ids)
         return -1;
     std::vector<int32_t> blk(static_cast<size_t>(cs) * n_stripes, 0);
@@ -142,7 +142,7 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
                   uint16_t* d_out, long long oss, long long ors,
                   long long words, int n_stripes, void* stream)
 {
-    if (!p || !d_ctx || !d_ids || !d_out || !d_coded || n_stripes < 0)
+    if (!p || !d_ctx || !d_ids || !d_out || !d_coded || n_stripes < 0 || words < 0)
         return -1;
     if (n_stripes == 0 || words == 0)
         return 0;
@@ -200,6 +200,18 @@ int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
                          n_stripes, d_counts ? &in : nullptr, 0, nullptr,
                          reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
                          cs, p->d_err, st(stream));
+}
+
+// git describe of the tree the library was built from + a hash of its
+// sources (quadiron_amd/csrc/Makefile writes QI_BUILD_ID), so a run's
+// record ties the loaded binary to a commit
+const char* qi_build_id(void)
+{
+#ifdef QI_BUILD_ID
+    return QI_BUILD_ID;
+#else
+    return "unknown";
+#endif
 }
 
 int qi_gpu_take_error(qi_plan* p)

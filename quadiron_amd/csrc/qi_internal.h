@@ -25,6 +25,11 @@ __host__ __device__ inline long long route_tiles(long long words)
     return (words + kRouteTile - 1) / kRouteTile;
 }
 
+// Sticky device error bits (qi_gpu_take_error): an OOR bucket held more
+// marks than its capacity `cap`, so some marks were lost (encode keeps the
+// exact count, decode could not restore every 65536 symbol).
+constexpr uint32_t kErrOorTruncated = 1u;
+
 // Row source for the matrix kernel: fragment `id` of stripe `s` is at
 //   id <  split : base0 + s*ss0 + id*rs0
 //   id >= split : base1 + s*ss1 + (id-split)*rs1        (elements of u16)
@@ -86,7 +91,8 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long mat_stride,
 int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
                       const uint16_t* d_ids, int n_stripes, int32_t* d_ctx,
                       long long ctx_stride, const Oor* in_oor, int slot_base,
-                      int by_pos, long long words, hipStream_t stream);
+                      int by_pos, long long words, uint32_t* d_err,
+                      hipStream_t stream);
 
 // matrix kernel instantiation choice
 int matrix_kp(int kin);

@@ -1,8 +1,12 @@
 """Multi-GPU path on CPU: bench.py's stripe sharding and its only
 collectives (MAX of the timed region, AND of the round-trip checks), run as
-2 gloo ranks.  The GPU bench uses the same functions over RCCL."""
+2 gloo ranks, and bench.py's own rank launcher (`--gpus N` -> N processes)
+in its device-free dry-run mode.  The GPU bench uses the same code over
+RCCL."""
+import json
 import os
 import socket
+import subprocess
 import sys
 
 import pytest
@@ -57,3 +61,41 @@ def test_sharded_bench_reductions(world):
         assert el2 == 0.5 and ok2 is False  # one failing rank fails all
         per_stripe = (16 + 64) * 2 * 32768 + 2 * 16 * 2 * 32768
         assert v == pytest.approx(world * 4096 * 10 * per_stripe / el / 1e9)
+
+
+def _bench(args, env_extra=None, timeout=300):
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                          capture_output=True, text=True, env=env,
+                          timeout=timeout, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_launches_n_ranks(n):
+    """`bench.py --gpus N` (no launcher around it) starts N ranks itself
+    before anything touches HIP, and rank 0 reports the process group's
+    size -- the dry run takes the same launch/shard/reduce path on gloo."""
+    r = _bench(["--gpus", str(n), "--dry-run", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n
+    assert out["dry_run"] is True and out["roundtrip_ok"] is True
+    assert out["scaling"] == "weak"
+    assert out["config"]["parallelism"] == f"stripe-sharded x{n} (no collective)"
+    per = (16 + 64) * 2 * 32768 + 2 * 16 * 2 * 32768
+    assert out["value"] == pytest.approx(
+        n * 4096 * 2 * per / (out["ms_per_step"] * 2e-3) / 1e9, rel=1e-6)
+
+
+def test_bench_world_mismatch_fails():
+    """--gpus N under a launcher whose world size differs is an error, not a
+    silent run on fewer GPUs."""
+    r = _bench(["--gpus", "2", "--dry-run", "--steps", "1", "--warmup", "0"],
+               {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr

@@ -325,6 +325,97 @@ def test_dense_oor_tile_uses_bucket_scan(k, m):
     assert torch.equal(dec, dd)
 
 
+def _dense_tile_setup(k, m, n_marks, P=2048, seed=99):
+    """Data whose encoding has ~n_marks OOR marks on the received rows
+    0..k-1 inside the first 1024-column tile."""
+    torch = _torch()
+    import quadiron_amd as qa
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 65536, (1, k, P), dtype=np.uint16)
+    _craft(k, m, 0, data[0], rng, n_marks, rows=range(k), col_range=(0, 1024))
+    plan = qa.Plan(k, m, False)
+    dd = torch.from_numpy(data.view(np.int16)).cuda()
+    out = torch.zeros((1, plan.n_outputs, P), dtype=torch.int16, device="cuda")
+    return plan, dd, out, P
+
+
+@pytest.mark.parametrize("k,m", [(16, 48), (32, 32), (100, 28)])
+def test_dense_tile_over_scratch_decodes(k, m):
+    """More than kMaxTileOor (256) marks of the received rows in ONE column
+    tile: the reference has no such limit, and neither does the decode --
+    the tile takes the slow bucket-walking path instead of failing (k=16:
+    matrix cores KS=1, k=32: KS=2, k=100: dot2 kernel)."""
+    torch = _torch()
+    plan, dd, out, P = _dense_tile_setup(k, m, 600)
+    cap = 1024
+    no = plan.n_outputs
+    counts = torch.zeros(no, dtype=torch.int32, device="cuda")
+    entries = torch.zeros(no * cap, dtype=torch.int32, device="cuda")
+    plan.encode(dd, out, counts, entries, cap)
+    torch.cuda.synchronize()
+    cnt = counts.cpu().numpy()
+    assert cnt[:k].sum() > 300, cnt[:k]
+    assert cnt.max() <= cap
+    ids = np.arange(k, dtype=np.uint16)[None, :]
+    di = torch.from_numpy(ids.view(np.int16)).cuda()
+    ctx = torch.zeros(plan.ctx_bytes(1, P), dtype=torch.uint8, device="cuda")
+    plan.decode_ctx(di, ctx, P, counts, entries, cap, h_ids=ids)
+    dec = torch.zeros_like(dd)
+    assert plan.decode(ctx, di, out, dec, counts=counts, entries=entries,
+                       cap=cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec, dd)
+
+
+@pytest.mark.parametrize("k,m", [(16, 48), (100, 28)])
+def test_decode_bucket_overflow_raises(k, m):
+    """A decode reading an OOR bucket whose count exceeds its capacity lost
+    marks: it must raise the plan's sticky error, not return wrong data
+    silently (the reference returns -1 on header overflow,
+    src/property.h:106-108)."""
+    torch = _torch()
+    plan, dd, out, P = _dense_tile_setup(k, m, 200, seed=5)
+    cap = 2
+    no = plan.n_outputs
+    counts = torch.zeros(no, dtype=torch.int32, device="cuda")
+    entries = torch.zeros(no * cap, dtype=torch.int32, device="cuda")
+    plan.encode(dd, out, counts, entries, cap)
+    torch.cuda.synchronize()
+    assert counts.cpu().numpy()[:k].max() > cap  # exact counts past cap
+    assert plan.take_error() == 0
+    ids = np.arange(k, dtype=np.uint16)[None, :]
+    di = torch.from_numpy(ids.view(np.int16)).cuda()
+    ctx = torch.zeros(plan.ctx_bytes(1, P), dtype=torch.uint8, device="cuda")
+    plan.decode_ctx(di, ctx, P, counts, entries, cap, h_ids=ids)
+    dec = torch.zeros_like(dd)
+    assert plan.decode(ctx, di, out, dec, counts=counts, entries=entries,
+                       cap=cap) != 0
+    assert plan.take_error() == 0  # reset by reading
+
+
+def test_plan_argument_checks():
+    """The Python wrapper refuses tensors the C-ABI would mis-address."""
+    torch = _torch()
+    import quadiron_amd as qa
+    plan = qa.Plan(16, 48)
+    good = torch.zeros((2, 16, 256), dtype=torch.int16, device="cuda")
+    out = torch.zeros((2, 64, 256), dtype=torch.int16, device="cuda")
+    with pytest.raises(TypeError):
+        plan.encode(good.float(), out)
+    with pytest.raises(TypeError):
+        plan.encode(good.cpu(), out)
+    with pytest.raises(ValueError):
+        plan.encode(good[:, :8], out)
+    with pytest.raises(ValueError):
+        plan.encode(good.transpose(1, 2).contiguous().transpose(1, 2), out)
+    with pytest.raises(ValueError):
+        plan.encode(good, out[:, :32])
+    cnt = torch.zeros(2 * 64, dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError):
+        plan.encode(good, out, cnt, torch.zeros(10, dtype=torch.int32,
+                                                device="cuda"), 64)
+
+
 # ------------------------------------------------------------------- RS-NF4
 
 def _nf4_roundtrip(ws, k, m, data, cap, missing):

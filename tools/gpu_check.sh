@@ -9,7 +9,7 @@ rm -f $O/pytest_gpu.log $O/membw2.log $O/bench*.log $O/host_rate.log
 timeout -k 10 400 python3 -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1 &&
 timeout -k 10 120 ./build/membw2 4096 > $O/membw2.log 2>&1 &&
 timeout -k 10 300 python3 bench.py --no-cpu-baseline > $O/bench.log 2>&1 &&
-timeout -k 10 300 python3 bench.py --cfg cfg3 --cpu-stripes 20 > $O/bench_cfg3.log 2>&1 &&
-timeout -k 10 300 python3 bench.py --systematic --cpu-stripes 50 > $O/bench_sys.log 2>&1
+timeout -k 10 300 python3 bench.py --cfg cfg3 > $O/bench_cfg3.log 2>&1 &&
+timeout -k 10 300 python3 bench.py --systematic > $O/bench_sys.log 2>&1
 rc=$?
 [ $rc -eq 0 ] && timeout -k 10 300 python3 tools/host_rate.py > $O/host_rate.log 2>&1
