@@ -293,7 +293,8 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
     check_rc(launch_matrix(L, ctx, 0, ctx + L.words(), 0, src, dst,
                            static_cast<long long>(words), 1, &in, 0, nullptr,
                            reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
-                           0, plan_->d_err, s),
+                           0, ctx_slow(plan_, h.ctx.p, static_cast<long long>(words)),
+                           plan_->d_err, s),
              "decode");
     for (int t = 0; t < k; t++)
         if (outputs[t])

@@ -410,6 +410,27 @@ struct MatExt {
     long long c0;
 };
 
+// everything a matrix launch needs (one kernel argument block)
+struct MatArgs {
+    MatLayout L;
+    const int32_t* mat;  // per-stripe matrix blocks, ms words apart (0: shared)
+    long long ms;
+    const int32_t* ids;  // per-stripe int32 ids, is apart (nullptr: identity)
+    long long is;
+    RowSrc src;
+    RowDst dst;
+    MatExt ext;
+    long long words;
+    int tiles;
+    Oor in_oor;  // input marks (counts nullptr: none)
+    int slot_base;
+    Oor out_oor;  // output marks recorded (counts nullptr: none)
+    const uint32_t* route;
+    long long rstride;
+    SlowList slow;
+    uint32_t* err;
+};
+
 // Where the OOR marks of the received rows (decode_prepare's restore of
 // 65536, src/fec_base.h:1361-1404) come from in a matrix launch.  A tile
 // normally takes them from the context's route table or from one scan of
@@ -423,27 +444,133 @@ struct OorScan {
     bool slow;
 };
 
-// f(position, word offset) for every mark of the received rows; a bucket
-// whose count exceeds its capacity lost entries on the way in: sticky
-// error kErrOorTruncated (the result of that stripe is not trustworthy)
-template <typename F>
-__device__ __forceinline__ void for_each_bucket_mark(const OorScan& sc, uint32_t* err,
-                                                     F f)
+// A tile with more than kMaxTileOor marks (adversarial data; the reference
+// has no such limit): the matrix kernels applied only the first
+// kMaxTileOor of them and appended the tile to its stripe's slow list (in
+// the decode context); matrix_redo_kernel, launched right after them on the
+// same stream, recomputes every column of the tile that holds a mark from
+// scratch -- all marks of the column restored, plain canonical arithmetic
+// -- and stores it again.  A column with several marks is recomputed by
+// several threads, which write the same words.  Only decodes carry input
+// marks, and their outputs are data symbols (< 65536), so nothing is
+// recorded as OOR here.  Keeping this out of the hot kernels keeps their
+// registers: inlined at their end it held the bucket and row pointers live
+// across the MFMA loop (SGPR spills, 2x slower decode).
+__device__ __forceinline__ void push_slow_tile(const SlowList& sl, int s, long long col0,
+                                               int width)
 {
-    for (int i = 0; i < sc.kin; i++) {
+    uint32_t* l = sl.base + s * sl.stride;
+    const uint32_t idx = atomicAdd(l, 1u);
+    l[1 + idx] = static_cast<uint32_t>(col0 / 256) << 2 |
+                 static_cast<uint32_t>(ilog2c(static_cast<uint32_t>(width / 256)));
+}
+
+__device__ void redo_marked_columns(const MatLayout& L, const int32_t* M,
+                                                 const RowSrc& src, const RowDst& dst,
+                                                 const OorScan& sc, long long col0,
+                                                 long long col1)
+{
+    const int kin = L.kin;
+    const int32_t* rscale = M + L.rscale();
+    const int32_t* plain = M + L.plain();
+    auto row_of = [&](int i) -> const uint16_t* {
+        const int id = src.by_pos ? i : (sc.sid ? sc.sid[i] : i);
+        return id < src.split ? src.base0 + sc.s * src.ss0 + id * src.rs0
+                              : src.base1 + sc.s * src.ss1 + (id - src.split) * src.rs1;
+    };
+    auto slot_of = [&](int i) {
         const int id = sc.sid ? sc.sid[i] : i;
-        const int slot = (sc.by_pos ? i : id) - sc.slot_base;
+        return (sc.by_pos ? i : id) - sc.slot_base;
+    };
+    // walk every mark (i, e) of the tile, one per thread
+    int base = 0;
+    for (int i = 0; i < kin; i++) {
+        const int slot = slot_of(i);
         if (slot < 0)
             continue;
         const long long bk = static_cast<long long>(sc.s) * sc.in.slots + slot;
-        uint32_t c = sc.in.counts[bk];
-        if (c > static_cast<uint32_t>(sc.in.cap)) {
-            if (err)
-                atomicOr(err, kErrOorTruncated);
-            c = static_cast<uint32_t>(sc.in.cap);
+        const int cnt = static_cast<int>(min(sc.in.counts[bk],
+                                             static_cast<uint32_t>(sc.in.cap)));
+        for (int e = static_cast<int>(threadIdx.x) - base; e < cnt;
+             e += static_cast<int>(blockDim.x)) {
+            if (e < 0)
+                continue;
+            const long long w = sc.in.entries[bk * sc.in.cap + e];
+            if (w < col0 || w >= col1)
+                continue;
+            for (int t = 0; t < L.R; t++) {
+                uint64_t acc = 0;
+                for (int j = 0; j < kin; j++) {
+                    uint32_t x = row_of(j)[w];
+                    const int sj = slot_of(j);
+                    if (sj >= 0) {  // restored 65536 at every mark of column w
+                        const long long bj = static_cast<long long>(sc.s) * sc.in.slots + sj;
+                        const uint32_t cj = min(sc.in.counts[bj],
+                                                static_cast<uint32_t>(sc.in.cap));
+                        for (uint32_t f = 0; f < cj; f++)
+                            if (sc.in.entries[bj * sc.in.cap + f] == w)
+                                x = 65536u;
+                    }
+                    acc += static_cast<uint64_t>(static_cast<uint32_t>(plain[t * kin + j])) * x;
+                }
+                uint32_t y = static_cast<uint32_t>(acc % 65537u);
+                const int32_t rs = rscale[t];
+                if (rs != 1)
+                    y = static_cast<uint32_t>(
+                        static_cast<uint64_t>(y) * static_cast<uint32_t>(rs < 0 ? rs + kQ : rs) %
+                        65537u);
+                dst.base[sc.s * dst.ss + t * dst.rs + w] =
+                    static_cast<uint16_t>(y == 65536u ? 0u : y);
+            }
         }
-        for (uint32_t e = 0; e < c; e++)
-            f(i, sc.in.entries[bk * sc.in.cap + e]);
+        base = (base + cnt) % static_cast<int>(blockDim.x);
+    }
+}
+
+// see push_slow_tile: one block per stripe at a time; the stripe's list is
+// emptied afterwards (a context can serve several decodes)
+__global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_stripes)
+{
+    const MatLayout L = a.L;
+    const int32_t* __restrict__ mat = a.mat;
+    const long long mat_stride = a.ms;
+    const int32_t* __restrict__ ids = a.ids;
+    const long long ids_stride = a.is;
+    const RowSrc src = a.src;
+    const RowDst dst = a.dst;
+    const MatExt ext = a.ext;
+    const long long words = a.words;
+    const int tiles = a.tiles;
+    const Oor in_oor = a.in_oor;
+    const int slot_base = a.slot_base;
+    const Oor out_oor = a.out_oor;
+    const uint32_t* __restrict__ route = a.route;
+    const long long route_stride = a.rstride;
+    const SlowList slow = a.slow;
+    uint32_t* err = a.err;
+    (void)ext;
+    (void)tiles;
+    (void)out_oor;
+    (void)route;
+    (void)route_stride;
+    (void)err;
+    for (int s = blockIdx.x; s < n_stripes; s += gridDim.x) {
+        uint32_t* l = slow.base + s * slow.stride;
+        const uint32_t n = __hip_atomic_load(l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n == 0)
+            continue;  // block-uniform
+        const OorScan sc{in_oor, ids ? ids + s * ids_stride : nullptr, src.by_pos,
+                         slot_base, L.kin, s, true};
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t code = l[1 + i];
+            const long long col0 = static_cast<long long>(code >> 2) * 256;
+            const long long col1 = col0 + (256LL << (code & 3));
+            redo_marked_columns(L, mat + s * mat_stride, src, dst, sc, col0,
+                                col1 < words ? col1 : words);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            *l = 0;
     }
 }
 
@@ -543,7 +670,7 @@ __device__ __forceinline__ void matrix_compute(
     const int32_t (&xp)[COLS][KP], const Region<BUF>& go, uint32_t ors,
     uint32_t voff, long long col, long long col0, long long avail, int s,
     int n_rm, const uint32_t* rm, int n_lm, const int* s_i,
-    const uint32_t* s_col, const OorScan& sc, uint32_t* err, const Oor& out_oor)
+    const uint32_t* s_col, const Oor& out_oor)
 {
     // M: the per-stripe matrix block (wave-uniform: scalar loads)
     const int kin = L.kin;
@@ -582,17 +709,12 @@ __device__ __forceinline__ void matrix_compute(
                         y[c] = fold(fold(y[c] - corr));
             }
         };
-        if (sc.slow) {  // block-uniform, rare
-            for_each_bucket_mark(sc, nullptr,
-                                 [&](int pos, uint32_t w) { restore(pos, w); });
-        } else {
-            for (int e = 0; e < n_rm + n_lm; e++) {
-                if (e < n_rm) {
-                    const uint32_t v = rm[e];
-                    restore(static_cast<int>(v >> 16), rbase + (v & 0xffffu));
-                } else {
-                    restore(s_i[e - n_rm], s_col[e - n_rm]);
-                }
+        for (int e = 0; e < n_rm + n_lm; e++) {
+            if (e < n_rm) {
+                const uint32_t v = rm[e];
+                restore(static_cast<int>(v >> 16), rbase + (v & 0xffffu));
+            } else {
+                restore(s_i[e - n_rm], s_col[e - n_rm]);
             }
         }
         const int32_t rs = rscale[t];
@@ -622,13 +744,25 @@ __device__ __forceinline__ void matrix_compute(
 }
 
 template <int KP, int COLS, bool BUF>
-__global__ __launch_bounds__(kBlock) void matrix_kernel(
-    MatLayout L, const int32_t* __restrict__ mat, long long mat_stride,
-    const int32_t* __restrict__ ids, long long ids_stride, RowSrc src,
-    RowDst dst, MatExt ext, long long words, int tiles, Oor in_oor,
-    int slot_base, Oor out_oor, const uint32_t* __restrict__ route,
-    long long route_stride, uint32_t* err)
+__global__ __launch_bounds__(kBlock) void matrix_kernel(MatArgs a)
 {
+    const MatLayout L = a.L;
+    const int32_t* __restrict__ mat = a.mat;
+    const long long mat_stride = a.ms;
+    const int32_t* __restrict__ ids = a.ids;
+    const long long ids_stride = a.is;
+    const RowSrc src = a.src;
+    const RowDst dst = a.dst;
+    const MatExt ext = a.ext;
+    const long long words = a.words;
+    const int tiles = a.tiles;
+    const Oor in_oor = a.in_oor;
+    const int slot_base = a.slot_base;
+    const Oor out_oor = a.out_oor;
+    const uint32_t* __restrict__ route = a.route;
+    const long long route_stride = a.rstride;
+    const SlowList slow = a.slow;
+    uint32_t* err = a.err;
     __shared__ int s_cnt;
     __shared__ int s_i[kMaxTileOor];
     __shared__ uint32_t s_col[kMaxTileOor];
@@ -699,18 +833,20 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(
     if (scan) {  // block-uniform
         const int cnt = scan_tile_marks(sc, col0, col1, words, &s_cnt, s_i, s_col, err);
         sc.slow = cnt > kMaxTileOor;
-        n_lm = sc.slow ? 0 : cnt;
+        n_lm = min(cnt, kMaxTileOor);
     }
     const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
     if (full) {
         matrix_compute<KP, COLS, true, BUF>(L, M, xp, go, ors, voff, col, col0,
                                             COLS, s, n_rm, rm, n_lm, s_i, s_col,
-                                            sc, err, out_oor);
+                                            out_oor);
     } else if (col < words) {
         matrix_compute<KP, COLS, false, BUF>(L, M, xp, go, ors, voff, col, col0,
                                              words - col, s, n_rm, rm, n_lm, s_i,
-                                             s_col, sc, err, out_oor);
+                                             s_col, out_oor);
     }
+    if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
+        push_slow_tile(slow, s, col0, kBlock * COLS);
 }
 
 // ---------------------------------------------------------------------------
@@ -762,13 +898,25 @@ struct MfmaTile {
 };
 
 template <int KS, int COLS>
-__global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
-    MatLayout L, const int32_t* __restrict__ mat, long long mat_stride,
-    const int32_t* __restrict__ ids, long long ids_stride, RowSrc src,
-    RowDst dst, MatExt ext, long long words, int tiles, Oor in_oor,
-    int slot_base, Oor out_oor, const uint32_t* __restrict__ route,
-    long long route_stride, uint32_t* err)
+__global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
 {
+    const MatLayout L = a.L;
+    const int32_t* __restrict__ mat = a.mat;
+    const long long mat_stride = a.ms;
+    const int32_t* __restrict__ ids = a.ids;
+    const long long ids_stride = a.is;
+    const RowSrc src = a.src;
+    const RowDst dst = a.dst;
+    const MatExt ext = a.ext;
+    const long long words = a.words;
+    const int tiles = a.tiles;
+    const Oor in_oor = a.in_oor;
+    const int slot_base = a.slot_base;
+    const Oor out_oor = a.out_oor;
+    const uint32_t* __restrict__ route = a.route;
+    const long long route_stride = a.rstride;
+    const SlowList slow = a.slow;
+    uint32_t* err = a.err;
     using G = MfmaTile<KS, COLS>;
     constexpr int NCOL = G::kCols, KH = G::kRows, RSB = G::kPitch;
     // one dynamic region (16-byte aligned base: no static LDS in front)
@@ -893,7 +1041,7 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
     if (scan) {  // block-uniform; the scan's barriers also publish the image
         const int cnt = scan_tile_marks(sc, col0, col1, words, s_cnt, s_i, s_col, err);
         sc.slow = cnt > kMaxTileOor;
-        n_lm = sc.slow ? 0 : cnt;
+        n_lm = min(cnt, kMaxTileOor);
     } else {
         __syncthreads();
     }
@@ -983,17 +1131,12 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
                             y[c] = fold(fold(y[c] - corr));
                 }
             };
-            if (sc.slow) {  // block-uniform, rare
-                for_each_bucket_mark(sc, nullptr,
-                                     [&](int pos, uint32_t wc) { restore(pos, wc); });
-            } else {
-                for (int e = 0; e < n_rm + n_lm; e++) {
-                    if (e < n_rm) {
-                        const uint32_t v = rm[e];
-                        restore(static_cast<int>(v >> 16), rbase + (v & 0xffffu));
-                    } else {
-                        restore(s_i[e - n_rm], s_col[e - n_rm]);
-                    }
+            for (int e = 0; e < n_rm + n_lm; e++) {
+                if (e < n_rm) {
+                    const uint32_t v = rm[e];
+                    restore(static_cast<int>(v >> 16), rbase + (v & 0xffffu));
+                } else {
+                    restore(s_i[e - n_rm], s_col[e - n_rm]);
                 }
             }
             if (__builtin_amdgcn_ballot_w64(rs != 1)) {
@@ -1077,6 +1220,8 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(
             rs = rsn;
         }
     }
+    if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
+        push_slow_tile(slow, s, col0, NCOL);
 }
 
 // ---------------------------------------------------------------------------
@@ -1206,9 +1351,12 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         cids[i] = 0;
     const long long ntiles = route_tiles(words);
 
-    // route table: clear, then (after the barrier below) fill
+    // route table: clear, then (after the barrier below) fill; the
+    // slow-tile list behind it starts empty
     for (long long t = tid; t < ntiles; t += NT)
         route[t * kRouteStride] = 0;
+    if (tid == 0)
+        route[ntiles * kRouteStride] = 0;
     if (tid < k) {
         const uint32_t id = ids[static_cast<long long>(s) * k + tid];
         xs[tid] = powm(r, id);
@@ -1444,50 +1592,30 @@ int matrix_kp(int kin)
 }
 
 template <int KP, int COLS, bool BUF>
-static int mat_launch(const MatLayout& L, const int32_t* mat, long long ms,
-                      const int32_t* ids, long long is, RowSrc src, RowDst dst,
-                      MatExt ext,
-                      long long words, int S, Oor in_oor, int slot_base,
-                      Oor out_oor, const uint32_t* route, long long rstride,
-                      uint32_t* err, hipStream_t st)
+static int mat_launch(MatArgs a, int S, hipStream_t st)
 {
-    int tiles;
-    if (grid_for(words - ext.c0, COLS, S, &tiles))
+    if (grid_for(a.words - a.ext.c0, COLS, S, &a.tiles))
         return -1;
-    hipLaunchKernelGGL((matrix_kernel<KP, COLS, BUF>), dim3(tiles * S),
-                       dim3(kBlock), 0, st, L, mat, ms, ids, is, src, dst, ext,
-                       words, tiles, in_oor, slot_base, out_oor, route, rstride,
-                       err);
+    hipLaunchKernelGGL((matrix_kernel<KP, COLS, BUF>), dim3(a.tiles * S), dim3(kBlock), 0,
+                       st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 // columns per lane: 4 (b64 row loads) while the packed rows fit in
 // registers, 2 up to KP 16, else 1; cols 1 is also the flat (BUF=false) path
 template <int KP>
-static int mat_dispatch(int cols, const MatLayout& L, const int32_t* mat,
-                        long long ms, const int32_t* ids, long long is,
-                        RowSrc src, RowDst dst, MatExt ext, long long words,
-                        int S, Oor io, int slot_base, Oor oo,
-                        const uint32_t* route, long long rstride, uint32_t* err,
-                        hipStream_t st)
+static int mat_dispatch(int cols, const MatArgs& a, int S, hipStream_t st)
 {
-    const bool buf = ext.e0 && ext.eo && (!src.base1 || ext.e1);
+    const bool buf = a.ext.e0 && a.ext.eo && (!a.src.base1 || a.ext.e1);
     if (!buf)
-        return mat_launch<KP, 1, false>(L, mat, ms, ids, is, src, dst, ext,
-                                        words, S, io, slot_base, oo, route,
-                                        rstride, err, st);
+        return mat_launch<KP, 1, false>(a, S, st);
     if constexpr (KP <= 8)
         if (cols == 4)
-            return mat_launch<KP, 4, true>(L, mat, ms, ids, is, src, dst, ext,
-                                           words, S, io, slot_base, oo, route,
-                                           rstride, err, st);
+            return mat_launch<KP, 4, true>(a, S, st);
     if constexpr (KP <= 16)
         if (cols >= 2)
-            return mat_launch<KP, 2, true>(L, mat, ms, ids, is, src, dst, ext,
-                                           words, S, io, slot_base, oo, route,
-                                           rstride, err, st);
-    return mat_launch<KP, 1, true>(L, mat, ms, ids, is, src, dst, ext, words, S,
-                                   io, slot_base, oo, route, rstride, err, st);
+            return mat_launch<KP, 2, true>(a, S, st);
+    return mat_launch<KP, 1, true>(a, S, st);
 }
 
 // columns per lane of the matrix-core kernel: KS = 1 (k <= 16) 4, i.e.
@@ -1498,17 +1626,14 @@ static int mat_dispatch(int cols, const MatLayout& L, const int32_t* mat,
 constexpr int kMfmaCols1 = 4, kMfmaCols4 = 2;
 
 template <int KS, int COLS>
-static int mfma_launch(const MatLayout& L, const int32_t* mat, long long ms,
-                       const int32_t* ids, long long is, RowSrc src, RowDst dst,
-                       MatExt ext, long long words, long long wfull, int S,
-                       Oor io, int slot_base, Oor oo, const uint32_t* route,
-                       long long rstride, uint32_t* err, hipStream_t st)
+static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 {
     using G = MfmaTile<KS, COLS>;
     const long long t = wfull / G::kCols;
     if (t <= 0 || t * S > 0x7fffffffLL)
         return -1;
-    const size_t lds = L.RB() > 1 ? G::kLdsStaged : G::kLds;
+    a.tiles = static_cast<int>(t);
+    const size_t lds = a.L.RB() > 1 ? G::kLdsStaged : G::kLds;
     // dynamic LDS above 64 KiB needs opting in, once per device (a bit per
     // device; a race only repeats the idempotent call)
     static std::atomic<uint64_t> attr_done{0};
@@ -1526,33 +1651,22 @@ static int mfma_launch(const MatLayout& L, const int32_t* mat, long long ms,
             attr_done.fetch_or(bit, std::memory_order_release);
         }
     }
-    hipLaunchKernelGGL((matrix_mfma_kernel<KS, COLS>), dim3(t * S), dim3(kBlock),
-                       lds, st, L, mat, ms, ids, is, src, dst, ext, words,
-                       static_cast<int>(t), io, slot_base, oo, route, rstride,
-                       err);
+    hipLaunchKernelGGL((matrix_mfma_kernel<KS, COLS>), dim3(t * S), dim3(kBlock), lds, st,
+                       a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
-                  const int32_t* ids, long long is, RowSrc src, RowDst dst,
-                  long long words,
-                  int S, const Oor* in_oor, int slot_base, const Oor* out_oor,
-                  const uint32_t* route, long long rstride, uint32_t* err,
-                  hipStream_t st)
+static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
 {
-    Oor none{nullptr, nullptr, 0, 0};
-    Oor io = in_oor ? *in_oor : none;
-    Oor oo = out_oor ? *out_oor : none;
+    const MatLayout& L = a.L;
+    const RowSrc& src = a.src;
+    const RowDst& dst = a.dst;
+    const long long words = a.words;
     const bool a2 = aligned_for(2, src.base0, src.ss0, src.rs0, dst.ss, dst.rs) &&
                     (src.base1 == nullptr ||
                      aligned_for(2, src.base1, src.ss1, src.rs1, 0, 0)) &&
                     (reinterpret_cast<uintptr_t>(dst.base) % 4) == 0;
-    if (L.KP != matrix_kp(L.kin))
-        return -4;
-    MatExt ext{extent(src.rows0, src.rs0, words),
-               extent(src.rows1, src.rs1, words),
-               extent(L.R, dst.rs, words), 0};
-    const bool buf = ext.e0 && ext.eo && (!src.base1 || ext.e1);
+    const bool buf = a.ext.e0 && a.ext.eo && (!src.base1 || a.ext.e1);
     const bool a4 = a2 &&
                     aligned_for(4, src.base0, src.ss0, src.rs0, dst.ss, dst.rs) &&
                     (src.base1 == nullptr ||
@@ -1565,40 +1679,56 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
     if (L.KS() > 0 && buf && a4 && wfull > 0) {
         int rc;
         if (L.KS() == 1)
-            rc = mfma_launch<1, kMfmaCols1>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
-                                   S, io, slot_base, oo, route, rstride, err, st);
+            rc = mfma_launch<1, kMfmaCols1>(a, wfull, S, st);
         else if (L.KS() == 2)
-            rc = mfma_launch<2, 2>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
-                                   S, io, slot_base, oo, route, rstride, err, st);
+            rc = mfma_launch<2, 2>(a, wfull, S, st);
         else
-            rc = mfma_launch<4, kMfmaCols4>(L, mat, ms, ids, is, src, dst, ext, words, wfull,
-                                   S, io, slot_base, oo, route, rstride, err, st);
+            rc = mfma_launch<4, kMfmaCols4>(a, wfull, S, st);
         if (rc || wfull == words)
             return rc;
-        ext.c0 = wfull;
+        a.ext.c0 = wfull;
     }
     switch (L.KP) {
     case 2:
-        return mat_dispatch<2>(cols, L, mat, ms, ids, is, src, dst, ext, words,
-                               S, io, slot_base, oo, route, rstride, err, st);
+        return mat_dispatch<2>(cols, a, S, st);
     case 4:
-        return mat_dispatch<4>(cols, L, mat, ms, ids, is, src, dst, ext, words,
-                               S, io, slot_base, oo, route, rstride, err, st);
+        return mat_dispatch<4>(cols, a, S, st);
     case 8:
-        return mat_dispatch<8>(cols, L, mat, ms, ids, is, src, dst, ext, words,
-                               S, io, slot_base, oo, route, rstride, err, st);
+        return mat_dispatch<8>(cols, a, S, st);
     case 16:
-        return mat_dispatch<16>(cols, L, mat, ms, ids, is, src, dst, ext, words,
-                                S, io, slot_base, oo, route, rstride, err, st);
+        return mat_dispatch<16>(cols, a, S, st);
     case 32:
-        return mat_dispatch<32>(cols, L, mat, ms, ids, is, src, dst, ext, words,
-                                S, io, slot_base, oo, route, rstride, err, st);
+        return mat_dispatch<32>(cols, a, S, st);
     case 64:
-        return mat_dispatch<64>(cols, L, mat, ms, ids, is, src, dst, ext, words,
-                                S, io, slot_base, oo, route, rstride, err, st);
+        return mat_dispatch<64>(cols, a, S, st);
     default:
         return -3;
     }
+}
+
+int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
+                  const int32_t* ids, long long is, RowSrc src, RowDst dst,
+                  long long words, int S, const Oor* in_oor, int slot_base,
+                  const Oor* out_oor, const uint32_t* route, long long rstride,
+                  SlowList slow, uint32_t* err, hipStream_t st)
+{
+    if (L.KP != matrix_kp(L.kin))
+        return -4;
+    if (in_oor && !slow.base)
+        return -1;  // input marks need the slow-tile lists
+    const Oor none{nullptr, nullptr, 0, 0};
+    MatArgs a{L, mat, ms, ids, is, src, dst,
+              MatExt{extent(src.rows0, src.rs0, words), extent(src.rows1, src.rs1, words),
+                     extent(L.R, dst.rs, words), 0},
+              words, 0, in_oor ? *in_oor : none, slot_base, out_oor ? *out_oor : none,
+              route, rstride, in_oor ? slow : SlowList{nullptr, 0}, err};
+    const int rc = launch_matrix_kernels(a, S, st);
+    if (rc || !in_oor)
+        return rc;
+    // tiles with more marks than the kernels' LDS list: see push_slow_tile
+    const int grid = S < 1024 ? S : 1024;
+    hipLaunchKernelGGL(matrix_redo_kernel, dim3(grid), dim3(kBlock), 0, st, a, S);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,

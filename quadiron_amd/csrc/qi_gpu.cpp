@@ -32,7 +32,16 @@ long long ctx_stride(const qi_plan* p, long long words)
 {
     const MatLayout L = ctx_layout(p);
     return static_cast<long long>(L.words()) + 2 * L.KP +
-           route_tiles(words) * kRouteStride;
+           route_tiles(words) * kRouteStride + slow_words(words);
+}
+
+// the slow-tile lists of n contexts (behind each route table)
+SlowList ctx_slow(const qi_plan* p, const void* d_ctx, long long words)
+{
+    const MatLayout L = ctx_layout(p);
+    uint32_t* c = static_cast<uint32_t*>(const_cast<void*>(d_ctx));
+    return SlowList{c + L.words() + 2 * L.KP + route_tiles(words) * kRouteStride,
+                    ctx_stride(p, words)};
 }
 
 // Decode contexts for n_stripes stripes: interpolation matrices + OOR route
@@ -110,7 +119,7 @@ int qi_gpu_encode(qi_plan* p, const uint16_t* d_data, long long dss,
     RowSrc src{d_data, dss, drs, 1 << 30, nullptr, 0, 0, 0, p->k, 0};
     return launch_matrix(p->gen, p->d_gen, 0, nullptr, 0, src, out, words,
                          n_stripes, nullptr, 0, d_counts ? &oor : nullptr,
-                         nullptr, 0, p->d_err, st(stream));
+                         nullptr, 0, SlowList{nullptr, 0}, p->d_err, st(stream));
 }
 
 size_t qi_gpu_decode_ctx_bytes(const qi_plan* p, int n_stripes,
@@ -163,7 +172,7 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
                          n_stripes, d_counts ? &in : nullptr, p->sys ? p->k : 0,
                          nullptr,
                          reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
-                         cs, p->d_err, st(stream));
+                         cs, ctx_slow(p, d_ctx, words), p->d_err, st(stream));
 }
 
 int qi_gpu_decode_ctx_packed(qi_plan* p, const uint16_t* d_ids,
@@ -199,7 +208,7 @@ int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, 0, nullptr,
                          reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
-                         cs, p->d_err, st(stream));
+                         cs, ctx_slow(p, d_ctx, words), p->d_err, st(stream));
 }
 
 // git describe of the tree the library was built from + a hash of its

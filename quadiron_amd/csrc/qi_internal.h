@@ -59,6 +59,22 @@ struct Oor {
     int cap;
 };
 
+// Per-stripe list of the column tiles whose received-row OOR marks overflowed
+// the matrix kernels' LDS list (more than 256 in one tile; adversarial
+// data).  Kept in the decode context: word 0 = count, then one word per
+// tile (col0 / 256) << 2 | log2(width / 256).  Capacity slow_words(words) - 1
+// covers every tile of a stripe.  launch_matrix runs matrix_redo_kernel
+// over it right after the matrix kernels.
+struct SlowList {
+    uint32_t* base;  // stripe s at base + s * stride (nullptr: no input marks)
+    long long stride;
+};
+
+__host__ __device__ inline long long slow_words(long long words)
+{
+    return 1 + (words + 255) / 256;
+}
+
 // ---- launchers (kernels.hip) ----
 // non-systematic encode by twisted register-resident sub-NTTs
 int launch_encode_fnt(int k, int n, int n_out, const int32_t* d_twist,
@@ -74,19 +90,22 @@ int launch_encode_fnt(int k, int n, int n_out, const int32_t* d_twist,
 //     slot_base (ids < slot_base have no bucket)
 //   out_oor: record OOR outputs (nullptr = no recording; values stored as 0)
 //   route: per-stripe OOR routing tables (route_stride u32 apart), or null
+//   slow: per-stripe slow-tile lists (required when in_oor is given)
 int launch_matrix(const MatLayout& L, const int32_t* mat, long long mat_stride,
                   const int32_t* ids, long long ids_stride, RowSrc src,
                   RowDst dst, long long words,
                   int n_stripes, const Oor* in_oor, int slot_base,
                   const Oor* out_oor, const uint32_t* route,
-                  long long route_stride, uint32_t* d_err, hipStream_t stream);
+                  long long route_stride, SlowList slow, uint32_t* d_err,
+                  hipStream_t stream);
 
 // per-stripe decode matrices from fragment ids (S x k).
 //   mode 0: coefficient extraction (non-systematic: data = poly coefs)
 //   mode 1: evaluation at r^t, t < k (systematic: data = P(r^t))
 //   d_ctx: per stripe ctx_stride words: the MatLayout block, the k ids as
-//   int32, then the OOR route table (route_tiles(words) x kRouteStride u32)
-//   built from in_oor
+//   int32 (padded to 2 KP), the OOR route table (route_tiles(words) x
+//   kRouteStride u32) built from in_oor, then the slow-tile list
+//   (slow_words(words) u32, count cleared)
 //   (slot = by_pos ? position : id - slot_base); in_oor may be null.
 int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
                       const uint16_t* d_ids, int n_stripes, int32_t* d_ctx,

@@ -62,6 +62,7 @@ struct qi_plan;
 namespace qi {
 // per-stripe decode context stride (int32 words) and builder (qi_gpu.cpp)
 long long ctx_stride(const qi_plan* p, long long words);
+SlowList ctx_slow(const qi_plan* p, const void* d_ctx, long long words);
 int build_ctx(qi_plan* p, const uint16_t* d_ids, const uint16_t* h_ids,
               int n_stripes, const Oor* in, int slot_base, int by_pos,
               long long words, void* d_ctx, hipStream_t s);
