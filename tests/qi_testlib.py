@@ -127,3 +127,68 @@ def oracle_nf4_decode_blocks(ws, k, m, outputs, oor, flags, cnt, missing):
         C.byref(c), ws, ptrs(dec), ptrs(par), vp(oor), vp(flags), vp(cnt),
         C.c_uint32(oor.shape[1]), vp(missing), vp(wanted), C.c_size_t(B))
     return ok, np.stack(dec)
+
+
+def craft_oor_columns(k, m, sys_, data_rows, rng, n_cols, rows=None, col_range=None):
+    """Force some outputs to 65536 (OOR) by solving for data row 0
+    (optionally only on output `rows`, in columns `col_range`)."""
+    o = oracle()
+    c = codec(k, m, sys_)
+    first = k if sys_ else 0
+    cw = (C.c_uint32 * c.n)()
+    din = (C.c_uint32 * k)()
+    ctx = C.create_string_buffer(40000)
+    if sys_:
+        o.qo_ctx_init(C.byref(c), ctx, (C.c_uint32 * k)(*range(k)))
+
+    def enc(vals):
+        for t in range(k):
+            din[t] = int(vals[t])
+        o.qo_encode_column(C.byref(c), ctx if sys_ else None, din, cw)
+        return [cw[first + i] for i in range(c.n_outputs)]
+
+    a = enc([1] + [0] * (k - 1))
+    P = data_rows.shape[1]
+    lo, hi = col_range if col_range else (0, P)
+    for j in lo + rng.choice(hi - lo, min(n_cols, hi - lo), replace=False):
+        col = data_rows[:, j].astype(np.int64)
+        col[0] = 0
+        b = enc(col)
+        i = int(rng.choice(rows)) if rows is not None else int(
+            rng.integers(0, c.n_outputs))
+        if a[i] == 0:
+            continue
+        d0 = ((65536 - b[i]) % Q) * pow(a[i], Q - 2, Q) % Q
+        if d0 < 65536:
+            data_rows[0, j] = d0
+
+
+def chunk_windows(words, chunk=1 << 21, width=4096):
+    """Column windows [lo, hi) around the start, every stream-chunk boundary
+    and the tail of a `words`-column block."""
+    wins = {(0, min(words, width))}
+    for c in range(chunk, words, chunk):
+        wins.add((max(0, c - width // 2), min(words, c + width // 2)))
+        wins.add((c, min(words, c + width)))
+    wins.add((max(0, words - width), words))
+    return sorted(wins)
+
+
+def check_windows_vs_oracle(k, m, sys_, data, outs, oor, cnt, wins, missing=None,
+                            dec=None):
+    """The codes are column-independent, so a large block's outputs (and OOR
+    marks, and decode) can be pinned to the oracle window by window: `data`
+    (k, 2*words) bytes, `outs` the product's (n_outputs, >= 2*words) coded
+    bytes with OOR lists oor/cnt (absolute word offsets)."""
+    no = outs.shape[0]
+    for lo, hi in wins:
+        d = np.ascontiguousarray(data[:, 2 * lo:2 * hi])
+        o_out, o_oor, o_cnt = oracle_encode_blocks(k, m, sys_, d, 64 + (hi - lo))
+        assert (outs[:, 2 * lo:2 * hi] == o_out).all(), (lo, hi)
+        for i in range(no):
+            got = [int(w) - lo for w in oor[i, :cnt[i]] if lo <= w < hi]
+            assert got == [int(w) for w in o_oor[i, :o_cnt[i]]], (lo, hi, i)
+        if missing is not None:
+            ok, o_dec = oracle_decode_blocks(k, m, sys_, o_out, o_oor, o_cnt,
+                                             missing, d)
+            assert ok == 1 and (dec[:, 2 * lo:2 * hi] == o_dec).all(), (lo, hi)

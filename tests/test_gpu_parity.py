@@ -5,7 +5,8 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from qi_testlib import (Q, codec, golden_names, load, oracle,
+from qi_testlib import (Q, check_windows_vs_oracle, chunk_windows, codec,
+                        craft_oor_columns, golden_names, load, oracle,
                         oracle_decode_blocks, oracle_encode_blocks)
 
 pytestmark = pytest.mark.gpu
@@ -133,38 +134,7 @@ def test_cabi_errors(hip_lib):
 
 # ------------------------------------------- device batch API vs oracle
 
-def _craft(k, m, sys_, data_rows, rng, n_cols, rows=None, col_range=None):
-    """Force some outputs to 65536 (OOR) by solving for data row 0
-    (optionally only on output `rows`, in columns `col_range`)."""
-    o = oracle()
-    c = codec(k, m, sys_)
-    first = k if sys_ else 0
-    cw = (C.c_uint32 * c.n)()
-    din = (C.c_uint32 * k)()
-    ctx = C.create_string_buffer(40000)
-    if sys_:
-        o.qo_ctx_init(C.byref(c), ctx, (C.c_uint32 * k)(*range(k)))
-
-    def enc(vals):
-        for t in range(k):
-            din[t] = int(vals[t])
-        o.qo_encode_column(C.byref(c), ctx if sys_ else None, din, cw)
-        return [cw[first + i] for i in range(c.n_outputs)]
-
-    a = enc([1] + [0] * (k - 1))
-    P = data_rows.shape[1]
-    lo, hi = col_range if col_range else (0, P)
-    for j in lo + rng.choice(hi - lo, min(n_cols, hi - lo), replace=False):
-        col = data_rows[:, j].astype(np.int64)
-        col[0] = 0
-        b = enc(col)
-        i = int(rng.choice(rows)) if rows is not None else int(
-            rng.integers(0, c.n_outputs))
-        if a[i] == 0:
-            continue
-        d0 = ((65536 - b[i]) % Q) * pow(a[i], Q - 2, Q) % Q
-        if d0 < 65536:
-            data_rows[0, j] = d0
+_craft = craft_oor_columns
 
 
 def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
@@ -492,8 +462,9 @@ def test_nf4_bad_word_size(hip_lib):
 ])
 def test_streams_match_blocks(hip_lib, k, m, sys_, B):
     """encode/decode_streams_vertical (two-slot pinned pipeline over chunks)
-    give the block API's outputs and OOR marks, and decode back to the data
-    -- including crafted OOR columns in every chunk."""
+    give the block API's and the oracle's outputs and OOR marks, and decode
+    to the oracle's decode of the same fragments (== the data) -- including
+    crafted OOR columns in every chunk."""
     import quadiron_amd as qa
     rng = np.random.default_rng(B)
     data = rng.integers(0, 256, (k, B), dtype=np.uint8)
@@ -531,7 +502,14 @@ def test_streams_match_blocks(hip_lib, k, m, sys_, B):
         qa.ptr_array(dec))
     assert rc == 1
     if sys_ and not miss[:k].any():
+        check_windows_vs_oracle(k, m, sys_, data, outs, oor, cnt,
+                                chunk_windows(words))
         return  # data in clear: nothing decoded (src/fec_base.h:931-932)
     # an odd-sized stream's last coded word lost its high byte when written
     # (read_bytes), so only whole words decode back -- as in the reference
     assert (np.stack(dec)[:, :2 * words] == data[:, :2 * words]).all()
+    # and against the oracle, not only the block API: outputs, OOR lists and
+    # the decode, window by window (start, every chunk seam -- where the
+    # crafted OOR columns sit -- and the tail)
+    check_windows_vs_oracle(k, m, sys_, data, outs, oor, cnt,
+                            chunk_windows(words), miss, np.stack(dec))
