@@ -699,7 +699,17 @@ __device__ __forceinline__ void matrix_compute(
         for (int c = 0; c < COLS; c++)
             y[c] = fold(acc[c]);  // T-range
         // restored OOR symbols: 65536 == -1 where the stored word is 0
-        auto restore = [&](int pos, long long w) {
+        for (int e = 0; e < n_rm + n_lm; e++) {
+            long long w;
+            int pos;
+            if (e < n_rm) {
+                const uint32_t v = rm[e];
+                pos = static_cast<int>(v >> 16);
+                w = rbase + (v & 0xffffu);
+            } else {
+                pos = s_i[e - n_rm];
+                w = s_col[e - n_rm];
+            }
             const long long d = w - col;
             if (d >= 0 && d < COLS) {
                 const int32_t corr = plain[t * kin + pos];
@@ -707,14 +717,6 @@ __device__ __forceinline__ void matrix_compute(
                 for (int c = 0; c < COLS; c++)
                     if (c == d)
                         y[c] = fold(fold(y[c] - corr));
-            }
-        };
-        for (int e = 0; e < n_rm + n_lm; e++) {
-            if (e < n_rm) {
-                const uint32_t v = rm[e];
-                restore(static_cast<int>(v >> 16), rbase + (v & 0xffffu));
-            } else {
-                restore(s_i[e - n_rm], s_col[e - n_rm]);
             }
         }
         const int32_t rs = rscale[t];
@@ -1121,7 +1123,19 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
                                              acc[T][0][j]));
             // restored OOR symbols of the received rows: 65536 == -1 where
             // the stored word is 0 (decode_prepare, src/fec_base.h:1361-1404)
-            auto restore = [&](int pos, long long wc) {
+            // (kept as one loop body: written as a lambda, the compiler
+            // indexed y[] dynamically and moved it to scratch memory)
+            for (int e = 0; e < n_rm + n_lm; e++) {
+                long long wc;
+                int pos;
+                if (e < n_rm) {
+                    const uint32_t v = rm[e];
+                    pos = static_cast<int>(v >> 16);
+                    wc = rbase + (v & 0xffffu);
+                } else {
+                    pos = s_i[e - n_rm];
+                    wc = s_col[e - n_rm];
+                }
                 const long long d = wc - cb;
                 if (trow && d >= 0 && d < 16) {
                     const int32_t corr = plain[t * kin + pos];
@@ -1129,14 +1143,6 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
                     for (int c = 0; c < 16; c++)
                         if (c == d)
                             y[c] = fold(fold(y[c] - corr));
-                }
-            };
-            for (int e = 0; e < n_rm + n_lm; e++) {
-                if (e < n_rm) {
-                    const uint32_t v = rm[e];
-                    restore(static_cast<int>(v >> 16), rbase + (v & 0xffffu));
-                } else {
-                    restore(s_i[e - n_rm], s_col[e - n_rm]);
                 }
             }
             if (__builtin_amdgcn_ballot_w64(rs != 1)) {

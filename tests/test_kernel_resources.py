@@ -1,0 +1,54 @@
+"""CPU: the compiler's resource report of the gfx950 kernels
+(build/obj/kernels.res, written by quadiron_amd/csrc/Makefile).  A hot kernel
+that spills to scratch memory runs through memory instead of registers (a
+y[16] epilogue array once landed there and doubled the decode time), so
+scratch use is an error outside the listed rare paths."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RES = os.path.join(ROOT, "build", "obj", "kernels.res")
+
+# kernels allowed to use scratch: the adversarial-OOR recompute and the
+# K = 64 encode codelet (256 VGPRs at 2 waves/SIMD, 3-4 spilled registers;
+# 3 waves/SIMD spilled 280 and ran 20 % slower, profiles/r1_ab_k64_encode.txt)
+ALLOWED = ("matrix_redo_kernel", "encode_fnt_kernelILi64E")
+
+
+def kernels():
+    if not os.path.exists(RES):
+        pytest.skip("kernel resource report not built (make -C quadiron_amd/csrc)")
+    out, cur = {}, None
+    for line in open(RES):
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            out[cur] = {}
+            continue
+        m = re.search(r"remark:\s+([A-Za-z ]+?)(?: \[[^\]]*\])?: (\d+)", line)
+        if m and cur:
+            out[cur][m.group(1).strip()] = int(m.group(2))
+    return out
+
+
+def test_report_lists_the_hot_kernels():
+    ks = kernels()
+    for name in ("encode_fnt_kernel", "matrix_mfma_kernel", "matrix_kernel",
+                 "decode_ctx_kernel", "matrix_redo_kernel"):
+        assert any(name in k for k in ks), name
+
+
+def test_no_scratch_in_hot_kernels():
+    bad = {k: v.get("ScratchSize") for k, v in kernels().items()
+           if v.get("ScratchSize", 0) > 0 and not any(a in k for a in ALLOWED)}
+    assert not bad, bad
+
+
+def test_mfma_kernel_occupancy():
+    """The matrix-core kernels keep >= 4 waves per SIMD (their LDS images
+    allow 4 blocks of 4 waves per CU at k <= 16)."""
+    for k, v in kernels().items():
+        if "matrix_mfma_kernel" in k:
+            assert v.get("Occupancy", 0) >= 4, (k, v)
