@@ -574,6 +574,20 @@ __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_st
     }
 }
 
+// the context's routed marks of this tile (count <= kRouteCap, entries
+// pos << 16 | column in the kRouteTile tile) into the LDS list (s_i, s_col)
+__device__ __forceinline__ void stage_route_marks(const uint32_t* rm, int n_rm,
+                                                  long long col0, int* s_i,
+                                                  uint32_t* s_col)
+{
+    if (static_cast<int>(threadIdx.x) < n_rm) {
+        const uint32_t v = rm[threadIdx.x];
+        s_i[threadIdx.x] = static_cast<int>(v >> 16);
+        s_col[threadIdx.x] =
+            static_cast<uint32_t>(col0 / kRouteTile * kRouteTile + (v & 0xffffu));
+    }
+}
+
 // block-wide scan of the buckets into the LDS list (s_i, s_col) of the
 // marks inside columns [col0, col1); returns the number of marks found
 // (> kMaxTileOor: the list is incomplete, use the slow path)
@@ -669,8 +683,7 @@ __device__ __forceinline__ void matrix_compute(
     const MatLayout& L, const int32_t* __restrict__ M,
     const int32_t (&xp)[COLS][KP], const Region<BUF>& go, uint32_t ors,
     uint32_t voff, long long col, long long col0, long long avail, int s,
-    int n_rm, const uint32_t* rm, int n_lm, const int* s_i,
-    const uint32_t* s_col, const Oor& out_oor)
+    int n_lm, const int* s_i, const uint32_t* s_col, const Oor& out_oor)
 {
     // M: the per-stripe matrix block (wave-uniform: scalar loads)
     const int kin = L.kin;
@@ -678,8 +691,6 @@ __device__ __forceinline__ void matrix_compute(
     const int32_t* rscale = M + L.rscale();
     const int32_t* plain = M + L.plain();
     const bool rec = out_oor.counts != nullptr;
-    // routed marks are relative to their kRouteTile-column tile
-    const long long rbase = col0 / kRouteTile * kRouteTile;
     for (int t = 0; t < L.R; t++) {
         const int32_t* mrow = M + t * KP;
         int32_t acc[COLS];
@@ -699,24 +710,18 @@ __device__ __forceinline__ void matrix_compute(
         for (int c = 0; c < COLS; c++)
             y[c] = fold(acc[c]);  // T-range
         // restored OOR symbols: 65536 == -1 where the stored word is 0
-        for (int e = 0; e < n_rm + n_lm; e++) {
-            long long w;
-            int pos;
-            if (e < n_rm) {
-                const uint32_t v = rm[e];
-                pos = static_cast<int>(v >> 16);
-                w = rbase + (v & 0xffffu);
-            } else {
-                pos = s_i[e - n_rm];
-                w = s_col[e - n_rm];
-            }
+        for (int e = 0; e < n_lm; e++) {
+            const int pos = s_i[e];
+            const long long w = s_col[e];
+            // branch-free per lane, unconditional load consumed at once (see
+            // the matrix-core epilogue: a load under a divergent branch made
+            // the compiler drain vmcnt(0) after every row)
             const long long d = w - col;
-            if (d >= 0 && d < COLS) {
-                const int32_t corr = plain[t * kin + pos];
+            const int32_t corr = plain[t * kin + pos];
 #pragma unroll
-                for (int c = 0; c < COLS; c++)
-                    if (c == d)
-                        y[c] = fold(fold(y[c] - corr));
+            for (int c = 0; c < COLS; c++) {
+                const int32_t yc = fold(fold(y[c] - corr));
+                y[c] = d == c ? yc : y[c];
             }
         }
         const int32_t rs = rscale[t];
@@ -836,16 +841,19 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(MatArgs a)
         const int cnt = scan_tile_marks(sc, col0, col1, words, &s_cnt, s_i, s_col, err);
         sc.slow = cnt > kMaxTileOor;
         n_lm = min(cnt, kMaxTileOor);
+    } else if (n_rm > 0) {  // block-uniform: the routed marks into the same list
+        stage_route_marks(rm, n_rm, col0, s_i, s_col);
+        __syncthreads();
+        n_lm = n_rm;
     }
     const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
     if (full) {
         matrix_compute<KP, COLS, true, BUF>(L, M, xp, go, ors, voff, col, col0,
-                                            COLS, s, n_rm, rm, n_lm, s_i, s_col,
-                                            out_oor);
+                                            COLS, s, n_lm, s_i, s_col, out_oor);
     } else if (col < words) {
         matrix_compute<KP, COLS, false, BUF>(L, M, xp, go, ors, voff, col, col0,
-                                             words - col, s, n_rm, rm, n_lm, s_i,
-                                             s_col, out_oor);
+                                             words - col, s, n_lm, s_i, s_col,
+                                             out_oor);
     }
     if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
         push_slow_tile(slow, s, col0, kBlock * COLS);
@@ -899,7 +907,7 @@ struct MfmaTile {
     static constexpr size_t kLdsStaged = kLds + 4 * kStage;
 };
 
-template <int KS, int COLS>
+template <int KS, int COLS, bool RSPLIT>
 __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
 {
     const MatLayout L = a.L;
@@ -974,22 +982,26 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
             for (int ty = 0; ty < 3; ty++)
                 b[ks][ty] = *reinterpret_cast<const qi_v2i*>(
                     mf + ((rb * KS + ks) * 3 + ty) * 128 + l * 2);
-        const int t = 16 * rb + tl;
-        kt = t < L.R ? kmf[t] : 0;
-        rs = t < L.R ? rscale[t] : 1;
+        // unconditional loads (a clamped row), selected after: an exec-masked
+        // load leaves the compiler unsure how many vector-memory ops are in
+        // flight, and it then drains vmcnt further than needed
+        const int t = 16 * rb + tl, tc = t < L.R ? t : L.R - 1;
+        const int32_t k0 = kmf[tc], r0 = rscale[tc];
+        kt = t < L.R ? k0 : 0;
+        rs = t < L.R ? r0 : 1;
     };
     // tall matrices (RB >= waves per block, the encode generators): wave wv
     // takes row blocks wv, wv + 4, ... over all the block's super tiles, so
     // each wave fetches only its own operand tiles (4x fewer L2 operand
     // reads than every wave walking every row block); otherwise every wave
     // takes every row block over its own COLS super tiles
+    // (RSPLIT = RB >= NW, chosen by the launcher: with a compile-time count
+    // of super tiles the loop unrolls and the compiler knows how many stores
+    // are in flight, so its wait for the next operands does not drain them)
     constexpr int NW = kBlock / 64;
-    const bool rsplit = RB >= NW;  // uniform
+    constexpr bool rsplit = RSPLIT;
     const int rb0 = rsplit ? wv : 0, rbs = rsplit ? NW : 1;
-    const int nst = rsplit ? NW * COLS : COLS;
-    qi_v2i bop[KS][3];
-    int32_t kt, rs;
-    load_ops(rb0, bop, kt, rs);
+    constexpr int nst = rsplit ? NW * COLS : COLS;
 
     // stage the tile as byte planes h' (rows 0..KH-1) and l' (rows KH..),
     // all row loads issued back to back; rows past kin load a clamped row
@@ -1045,25 +1057,29 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
         sc.slow = cnt > kMaxTileOor;
         n_lm = min(cnt, kMaxTileOor);
     } else {
+        // the routed marks into the same LDS list: the epilogue then reads
+        // only LDS (no memory loads in the hot loop)
+        stage_route_marks(rm, n_rm, col0, s_i, s_col);
         __syncthreads();
+        n_lm = n_rm;
     }
 
     // matrix cores: wave wv covers COLS super tiles of 64 columns, for each
     // block of 16 output rows in turn (the next block's operands prefetched)
     const bool rec = out_oor.counts != nullptr;
-    const long long rbase = col0 / kRouteTile * kRouteTile;
     const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
     // generic -> LDS address space (C-style cast: reinterpret_cast cannot
     // change the address space)
     auto* lds = (__attribute__((address_space(3))) uint8_t*)img;
     const uint32_t abase = static_cast<uint32_t>((8 * g + q) * RSB + 8 * p);
-    for (int rb = rb0; rb < RB; rb += rbs) {
+    // One row block: every super tile's MFMAs, epilogue and stores, with
+    // the block's operand tiles b / kt / rs.
+    auto rb_body = [&](int rb, const qi_v2i (&bop)[KS][3], const int32_t kt,
+                       const int32_t rs) {
         const int t = 16 * rb + tl;
         const bool trow = t < L.R;
-        qi_v2i bnx[KS][3];
-        int32_t ktn = 0, rsn = 1;
-        if (rb + rbs < RB)
-            load_ops(rb + rbs, bnx, ktn, rsn);
+        const int tcl = trow ? t : L.R - 1;  // a valid row for the loads
+#pragma unroll 1
         for (int st = 0; st < nst; st++) {
             const int ST = rsplit ? st : wv * COLS + st;
             qi_v4i acc[4][3];
@@ -1123,26 +1139,23 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
                                              acc[T][0][j]));
             // restored OOR symbols of the received rows: 65536 == -1 where
             // the stored word is 0 (decode_prepare, src/fec_base.h:1361-1404)
-            // (kept as one loop body: written as a lambda, the compiler
-            // indexed y[] dynamically and moved it to scratch memory)
-            for (int e = 0; e < n_rm + n_lm; e++) {
-                long long wc;
-                int pos;
-                if (e < n_rm) {
-                    const uint32_t v = rm[e];
-                    pos = static_cast<int>(v >> 16);
-                    wc = rbase + (v & 0xffffu);
-                } else {
-                    pos = s_i[e - n_rm];
-                    wc = s_col[e - n_rm];
-                }
+            // Branch-free per lane: the marks come from LDS and the
+            // coefficient load is unconditional and consumed at once.  A gather load under a lane-divergent branch left a
+            // possibly pending load into a reused VGPR at the loop exit,
+            // and the compiler then drained vmcnt(0) -- every outstanding
+            // store and operand prefetch -- after every super tile, with or
+            // without marks (cfg3 encode: wait_any 34 % of wave cycles).
+            // (One loop body, no lambda: as a lambda the compiler indexed
+            // y[] dynamically and moved it to scratch memory.)
+            for (int e = 0; e < n_lm; e++) {
+                const int pos = s_i[e];
+                const long long wc = s_col[e];
                 const long long d = wc - cb;
-                if (trow && d >= 0 && d < 16) {
-                    const int32_t corr = plain[t * kin + pos];
+                const int32_t corr = plain[tcl * kin + pos];
 #pragma unroll
-                    for (int c = 0; c < 16; c++)
-                        if (c == d)
-                            y[c] = fold(fold(y[c] - corr));
+                for (int c = 0; c < 16; c++) {
+                    const int32_t yc = fold(fold(y[c] - corr));
+                    y[c] = (trow && d == c) ? yc : y[c];
                 }
             }
             if (__builtin_amdgcn_ballot_w64(rs != 1)) {
@@ -1202,29 +1215,43 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
             for (int h = 0; h < 2; h++) {
                 const int orow = 8 * h + (l >> 3), c = l & 7;
                 const qi_v4u v = *reinterpret_cast<const qi_v4u*>(at(orow, 16 * c));
+                // rows >= R get an offset past the buffer resource's extent
+                // (< 2^31): the hardware drops those stores.  Unconditional,
+                // so the compiler keeps an exact count of the stores in flight
                 const int ot = 16 * rb + orow;
-                if (ot < L.R) {
-                    const uint32_t vo =
-                        static_cast<uint32_t>(ot) * ors +
-                        static_cast<uint32_t>((col0 + 64 * ST + 8 * c) * 2);
-                    __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo),
-                                                           0, kAuxStMf);
-                }
+                const uint32_t vo =
+                    ot < L.R ? static_cast<uint32_t>(ot) * ors +
+                                   static_cast<uint32_t>((col0 + 64 * ST + 8 * c) * 2)
+                             : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo), 0,
+                                                       kAuxStMf);
             }
             // the staging tile is rewritten by the next (ST, rb): keep this
             // iteration's reads ahead of those writes
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
+            // unrolled super tiles stay apart (interleaved, they held every
+            // tile's accumulators at once: 256 VGPRs, 1 wave/SIMD)
+            __builtin_amdgcn_sched_barrier(0);
         }
-        if (rb + rbs < RB) {
-#pragma unroll
-            for (int ks = 0; ks < KS; ks++)
-#pragma unroll
-                for (int ty = 0; ty < 3; ty++)
-                    bop[ks][ty] = bnx[ks][ty];
-            kt = ktn;
-            rs = rsn;
-        }
+    };
+    // Row blocks in ping-pong over two operand buffers, each prefetch one row
+    // block ahead and unconditional (a clamped row block past the end).  On
+    // gfx9 loads and stores share the in-order vmcnt: copying a prefetched
+    // buffer (or a conditional prefetch) made the compiler drain vmcnt(0) at
+    // every row block -- i.e. wait for all the previous block's streaming
+    // stores before the next MFMA could issue.
+    qi_v2i bA[KS][3], bB[KS][3];
+    int32_t ktA, rsA, ktB, rsB;
+    load_ops(rb0, bA, ktA, rsA);
+    const int rlast = RB - 1;
+    for (int rb = rb0; rb < RB; rb += 2 * rbs) {
+        load_ops(min(rb + rbs, rlast), bB, ktB, rsB);
+        rb_body(rb, bA, ktA, rsA);
+        if (rb + rbs >= RB)
+            break;
+        load_ops(min(rb + 2 * rbs, rlast), bA, ktA, rsA);
+        rb_body(rb + rbs, bB, ktB, rsB);
     }
     if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
         push_slow_tile(slow, s, col0, NCOL);
@@ -1631,7 +1658,7 @@ static int mat_dispatch(int cols, const MatArgs& a, int S, hipStream_t st)
 // (profiles/r1_ab_mfma_cols1.txt).
 constexpr int kMfmaCols1 = 4, kMfmaCols4 = 2;
 
-template <int KS, int COLS>
+template <int KS, int COLS, bool RSPLIT>
 static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 {
     using G = MfmaTile<KS, COLS>;
@@ -1650,16 +1677,23 @@ static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
         const uint64_t bit = dev < 64 ? 1ull << dev : 0;
         if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
             if (hipFuncSetAttribute(
-                    reinterpret_cast<const void*>(&matrix_mfma_kernel<KS, COLS>),
+                    reinterpret_cast<const void*>(&matrix_mfma_kernel<KS, COLS, RSPLIT>),
                     hipFuncAttributeMaxDynamicSharedMemorySize,
                     static_cast<int>(G::kLdsStaged)) != hipSuccess)
                 return -2;
             attr_done.fetch_or(bit, std::memory_order_release);
         }
     }
-    hipLaunchKernelGGL((matrix_mfma_kernel<KS, COLS>), dim3(t * S), dim3(kBlock), lds, st,
+    hipLaunchKernelGGL((matrix_mfma_kernel<KS, COLS, RSPLIT>), dim3(t * S), dim3(kBlock), lds, st,
                        a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <int KS, int COLS>
+static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
+{
+    return a.L.RB() >= kBlock / 64 ? mfma_launch<KS, COLS, true>(a, wfull, S, st)
+                                   : mfma_launch<KS, COLS, false>(a, wfull, S, st);
 }
 
 static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
