@@ -892,11 +892,17 @@ typedef int qi_v4i __attribute__((ext_vector_type(4)));
 typedef int qi_v2i __attribute__((ext_vector_type(2)));
 typedef unsigned int qi_v4u __attribute__((ext_vector_type(4)));
 
-template <int KS, int COLS>
+// Geometry of a matrix-core block: NST super tiles of 64 columns (the
+// block's columns, staged once as the A image), NW waves.  RSPLIT: the waves
+// split the row blocks (wave wv takes wv, wv + NW, ...) and each walks every
+// super tile, so an operand tile is fetched once per block; otherwise every
+// wave takes every row block over its own NST / NW super tiles.
+template <int KS, int NST, int NW>
 struct MfmaTile {
-    static constexpr int kCols = kBlock * COLS;  // columns per block
-    static constexpr int kRows = 16 * KS;        // rows per byte plane
-    static constexpr int kPitch = kCols + 16;    // LDS row pitch: +4 banks/row
+    static constexpr int kThreads = 64 * NW;
+    static constexpr int kCols = 64 * NST;     // columns per block
+    static constexpr int kRows = 16 * KS;      // rows per byte plane
+    static constexpr int kPitch = kCols + 16;  // LDS row pitch: +4 banks/row
     static constexpr size_t kImg = static_cast<size_t>(2 * kRows) * kPitch;
     // image + OOR scan scratch (s_i, s_col) + s_cnt
     static constexpr size_t kLds = kImg + 2 * 4 * kMaxTileOor + 16;
@@ -904,11 +910,17 @@ struct MfmaTile {
     // allocated when the block has several 16-row output blocks
     static constexpr int kStagePitch = 144;
     static constexpr size_t kStage = 16 * kStagePitch;
-    static constexpr size_t kLdsStaged = kLds + 4 * kStage;
+    static constexpr size_t kLdsStaged = kLds + NW * kStage;
+    // staging loads: CPL columns per lane (b64 or b32), TPR lanes per image
+    // row, RG row groups
+    static constexpr int kCpl = kCols >= 4 * kThreads ? 4 : 2;
+    static constexpr int kTpr = kCols / kCpl;
+    static constexpr int kRg = kThreads / kTpr;
+    static_assert(kRg >= 1 && kThreads % kTpr == 0 && kRows % kRg == 0, "staging");
 };
 
-template <int KS, int COLS, bool RSPLIT>
-__global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
+template <int KS, int NST, int NW, bool RSPLIT>
+__global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
 {
     const MatLayout L = a.L;
     const int32_t* __restrict__ mat = a.mat;
@@ -927,8 +939,9 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
     const long long route_stride = a.rstride;
     const SlowList slow = a.slow;
     uint32_t* err = a.err;
-    using G = MfmaTile<KS, COLS>;
+    using G = MfmaTile<KS, NST, NW>;
     constexpr int NCOL = G::kCols, KH = G::kRows, RSB = G::kPitch;
+    constexpr int CPL = G::kCpl, RG = G::kRg;
     // one dynamic region (16-byte aligned base: no static LDS in front)
     extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
     uint8_t* img = qi_lds;
@@ -941,7 +954,9 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
     const int kin = L.kin;
     const long long col0 = static_cast<long long>(tile) * NCOL;
     const long long col1 = col0 + NCOL;
-    const uint32_t cl = threadIdx.x * COLS;  // this thread's first column
+    // staging: this thread's first column and its row group
+    const uint32_t cl = (RG == 1 ? threadIdx.x : threadIdx.x % G::kTpr) * CPL;
+    const int rg = RG == 1 ? 0 : static_cast<int>(threadIdx.x / G::kTpr);
     const uint32_t voff = static_cast<uint32_t>((col0 + cl) * 2);
     const int32_t* M = mat + s * mat_stride;
     const int32_t* sid = ids ? ids + s * ids_stride : nullptr;
@@ -990,27 +1005,23 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
         kt = t < L.R ? k0 : 0;
         rs = t < L.R ? r0 : 1;
     };
-    // tall matrices (RB >= waves per block, the encode generators): wave wv
-    // takes row blocks wv, wv + 4, ... over all the block's super tiles, so
-    // each wave fetches only its own operand tiles (4x fewer L2 operand
-    // reads than every wave walking every row block); otherwise every wave
-    // takes every row block over its own COLS super tiles
-    // (RSPLIT = RB >= NW, chosen by the launcher: with a compile-time count
-    // of super tiles the loop unrolls and the compiler knows how many stores
-    // are in flight, so its wait for the next operands does not drain them)
-    constexpr int NW = kBlock / 64;
+    // tall matrices (RSPLIT, the encode generators): wave wv takes row
+    // blocks wv, wv + NW, ... over all the block's super tiles, so each wave
+    // fetches only its own operand tiles (NW x fewer L2 operand reads than
+    // every wave walking every row block); otherwise every wave takes every
+    // row block over its own super tiles
     constexpr bool rsplit = RSPLIT;
     const int rb0 = rsplit ? wv : 0, rbs = rsplit ? NW : 1;
-    constexpr int nst = rsplit ? NW * COLS : COLS;
+    constexpr int nst = rsplit ? NST : NST / NW;
+    static_assert(rsplit || NST % NW == 0, "super tiles per wave");
 
-    // stage the tile as byte planes h' (rows 0..KH-1) and l' (rows KH..),
-    // all row loads issued back to back; rows past kin load a clamped row
-    // (their operand bytes are 0)
-    // COLS = 1: one u16 column per lane (256-column blocks: half the LDS
-    // image, for the KS = 4 kernels' occupancy)
-    uint32_t w[KH][COLS > 1 ? COLS / 2 : 1];
+    // stage the tile as byte planes h' (rows 0..KH-1) and l' (rows KH..):
+    // this thread's CPL columns of every RG-th row, all row loads issued back
+    // to back; rows past kin load a clamped row (their operand bytes are 0)
+    uint32_t w[KH / RG][CPL / 2];
 #pragma unroll
-    for (int i = 0; i < KH; i++) {
+    for (int r = 0; r < KH / RG; r++) {
+        const int i = r * RG + rg;
         const int ii = i < kin ? i : kin - 1;
         const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
         const bool lo = id < src.split;
@@ -1018,32 +1029,26 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
         g.r = lo ? g0.r : g1.r;
         const uint32_t off = static_cast<uint32_t>(
             lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
-        if constexpr (COLS == 1)
-            w[i][0] = __builtin_amdgcn_raw_buffer_load_b16(
-                g.r, static_cast<int>(voff), static_cast<int>(off), kAuxLd);
-        else
-            ld_dw<COLS / 2, true, kAuxLd>(g, off, voff, w[i]);
+        ld_dw<CPL / 2, true, kAuxLd>(g, off, voff, w[r]);
     }
     const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) +
                           4 * ((cl % 64) / 16) + cl % 4;
 #pragma unroll
-    for (int i = 0; i < KH; i++) {
-        if constexpr (COLS == 4) {
+    for (int r = 0; r < KH / RG; r++) {
+        const int i = r * RG + rg;
+        if constexpr (CPL == 4) {
             // [c0 lo, c0 hi, c1 lo, c1 hi] [c2 lo, ...] -> hi / lo planes
             const uint32_t hi =
-                __builtin_amdgcn_perm(w[i][1], w[i][0], 0x07050301u) ^ 0x80808080u;
+                __builtin_amdgcn_perm(w[r][1], w[r][0], 0x07050301u) ^ 0x80808080u;
             const uint32_t lo =
-                __builtin_amdgcn_perm(w[i][1], w[i][0], 0x06040200u) ^ 0x80808080u;
+                __builtin_amdgcn_perm(w[r][1], w[r][0], 0x06040200u) ^ 0x80808080u;
             *reinterpret_cast<uint32_t*>(img + i * RSB + lpos) = hi;
             *reinterpret_cast<uint32_t*>(img + (KH + i) * RSB + lpos) = lo;
-        } else if constexpr (COLS == 1) {
-            img[i * RSB + lpos] = static_cast<uint8_t>((w[i][0] >> 8) ^ 0x80u);
-            img[(KH + i) * RSB + lpos] = static_cast<uint8_t>(w[i][0] ^ 0x80u);
         } else {
             const uint32_t hi =
-                __builtin_amdgcn_perm(0u, w[i][0], 0x0c0c0301u) ^ 0x8080u;
+                __builtin_amdgcn_perm(0u, w[r][0], 0x0c0c0301u) ^ 0x8080u;
             const uint32_t lo =
-                __builtin_amdgcn_perm(0u, w[i][0], 0x0c0c0200u) ^ 0x8080u;
+                __builtin_amdgcn_perm(0u, w[r][0], 0x0c0c0200u) ^ 0x8080u;
             *reinterpret_cast<uint16_t*>(img + i * RSB + lpos) =
                 static_cast<uint16_t>(hi);
             *reinterpret_cast<uint16_t*>(img + (KH + i) * RSB + lpos) =
@@ -1064,7 +1069,7 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
         n_lm = n_rm;
     }
 
-    // matrix cores: wave wv covers COLS super tiles of 64 columns, for each
+    // matrix cores: wave wv covers nst super tiles of 64 columns, for each
     // block of 16 output rows in turn (the next block's operands prefetched)
     const bool rec = out_oor.counts != nullptr;
     const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
@@ -1081,7 +1086,7 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
         const int tcl = trow ? t : L.R - 1;  // a valid row for the loads
 #pragma unroll 1
         for (int st = 0; st < nst; st++) {
-            const int ST = rsplit ? st : wv * COLS + st;
+            const int ST = rsplit ? st : wv * nst + st;
             qi_v4i acc[4][3];
 #pragma unroll
             for (int T = 0; T < 4; T++) {
@@ -1230,9 +1235,6 @@ __global__ __launch_bounds__(kBlock) void matrix_mfma_kernel(MatArgs a)
             // iteration's reads ahead of those writes
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            // unrolled super tiles stay apart (interleaved, they held every
-            // tile's accumulators at once: 256 VGPRs, 1 wave/SIMD)
-            __builtin_amdgcn_sched_barrier(0);
         }
     };
     // Row blocks in ping-pong over two operand buffers, each prefetch one row
@@ -1651,17 +1653,10 @@ static int mat_dispatch(int cols, const MatArgs& a, int S, hipStream_t st)
     return mat_launch<KP, 1, true>(a, S, st);
 }
 
-// columns per lane of the matrix-core kernel: KS = 1 (k <= 16) 4, i.e.
-// 1024-column blocks, 35 KB LDS; KS = 2, 4: 2 (512 columns; at KS = 4 77 KB
-// LDS, 2 blocks/CU).  One u16 column per lane at KS = 4 (256 columns, 44 KB,
-// 3 blocks/CU) slowed the cfg3 decode 0.196 -> 0.205 ms
-// (profiles/r1_ab_mfma_cols1.txt).
-constexpr int kMfmaCols1 = 4, kMfmaCols4 = 2;
-
-template <int KS, int COLS, bool RSPLIT>
+template <int KS, int NST, int NW, bool RSPLIT>
 static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 {
-    using G = MfmaTile<KS, COLS>;
+    using G = MfmaTile<KS, NST, NW>;
     const long long t = wfull / G::kCols;
     if (t <= 0 || t * S > 0x7fffffffLL)
         return -1;
@@ -1677,23 +1672,37 @@ static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
         const uint64_t bit = dev < 64 ? 1ull << dev : 0;
         if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
             if (hipFuncSetAttribute(
-                    reinterpret_cast<const void*>(&matrix_mfma_kernel<KS, COLS, RSPLIT>),
+                    reinterpret_cast<const void*>(&matrix_mfma_kernel<KS, NST, NW, RSPLIT>),
                     hipFuncAttributeMaxDynamicSharedMemorySize,
                     static_cast<int>(G::kLdsStaged)) != hipSuccess)
                 return -2;
             attr_done.fetch_or(bit, std::memory_order_release);
         }
     }
-    hipLaunchKernelGGL((matrix_mfma_kernel<KS, COLS, RSPLIT>), dim3(t * S), dim3(kBlock), lds, st,
-                       a);
+    hipLaunchKernelGGL((matrix_mfma_kernel<KS, NST, NW, RSPLIT>), dim3(t * S),
+                       dim3(G::kThreads), lds, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <int KS, int COLS>
-static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
+// Block geometry by matrix shape (kRouteTile = 1024 must be a multiple of
+// the block width):
+//  - short matrices (RB < 4: decodes, k x k): 4 waves, each on its own super
+//    tiles; 1024 columns at KS = 1 (35 KB LDS), 512 at KS = 2, 4 (one u16
+//    column per lane at KS = 4 -- 256 columns -- slowed the cfg3 decode,
+//    profiles/r1_ab_mfma_cols1.txt);
+//  - tall ones (RB >= 4: encode generators): the waves split the row blocks
+//    over the whole image.  8 waves over 256 columns (54 KB LDS: 2 blocks =
+//    4 waves per SIMD instead of 2) measured slower on the 1024 x 64 cfg3
+//    generator (1.37 vs 1.22 ms, gpurun_out r2f), so the block stays at 4
+//    waves.
+template <int KS>
+static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t st)
 {
-    return a.L.RB() >= kBlock / 64 ? mfma_launch<KS, COLS, true>(a, wfull, S, st)
-                                   : mfma_launch<KS, COLS, false>(a, wfull, S, st);
+    constexpr int NSTS = KS == 1 ? 16 : 8;
+    const int RB = a.L.RB();
+    if (RB >= 4)
+        return mfma_launch<KS, NSTS, 4, true>(a, wfull, S, st);
+    return mfma_launch<KS, NSTS, 4, false>(a, wfull, S, st);
 }
 
 static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
@@ -1719,11 +1728,11 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
     if (L.KS() > 0 && buf && a4 && wfull > 0) {
         int rc;
         if (L.KS() == 1)
-            rc = mfma_launch<1, kMfmaCols1>(a, wfull, S, st);
+            rc = mfma_dispatch<1>(a, wfull, S, st);
         else if (L.KS() == 2)
-            rc = mfma_launch<2, 2>(a, wfull, S, st);
+            rc = mfma_dispatch<2>(a, wfull, S, st);
         else
-            rc = mfma_launch<4, kMfmaCols4>(a, wfull, S, st);
+            rc = mfma_dispatch<4>(a, wfull, S, st);
         if (rc || wfull == words)
             return rc;
         a.ext.c0 = wfull;
