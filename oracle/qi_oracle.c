@@ -170,8 +170,8 @@ void qo_fft_inv(int n, uint32_t w, const uint32_t* in, uint32_t* out)
 /* Codec plan: src/fec_rs_fnt.h:69-163 */
 int qo_codec_init(qo_codec* c, int k, int m, int sys)
 {
-    /* oracle limits: k <= 1024, k + m <= 2048 (fixed-size scratch) */
-    if (k < 1 || m < 1 || k > 1024 || k + m > 2048)
+    /* oracle limits: k <= QO_KMAX, k + m <= 65536 (fixed-size scratch) */
+    if (k < 1 || m < 1 || k > QO_KMAX || k + m > 65536)
         return -1;
     c->sys = sys ? 1 : 0;
     c->k = k;
@@ -192,7 +192,7 @@ int qo_ctx_init(const qo_codec* c, qo_ctx* ctx, const uint32_t* ids)
     int k = c->k, n = c->n, i, d;
     uint32_t *A, *Ad, *A_fft, *A2k;
 
-    if (k > 1024 || c->len_2k > 2048)
+    if (k > QO_KMAX || c->len_2k > 2 * QO_KMAX)
         return -1;
     A = (uint32_t*)calloc((size_t)n + 1, sizeof(uint32_t));
     Ad = (uint32_t*)calloc((size_t)n, sizeof(uint32_t));
@@ -272,7 +272,7 @@ void qo_decode_column(const qo_codec* c, const qo_ctx* ctx,
     if (c->sys) {
         /* fft(dec_inter_codeword, output); keep rows 0..k-1 */
         uint32_t* cw = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)c->n);
-        uint32_t tmp[1024];
+        uint32_t tmp[QO_KMAX];
         int i;
         for (i = 0; i < c->k; i++)
             tmp[i] = data[i];
@@ -288,7 +288,7 @@ void qo_encode_column(const qo_codec* c, const qo_ctx* enc_ctx,
                       const uint32_t* data, uint32_t* codeword)
 {
     if (c->sys) {
-        uint32_t inter[1024];
+        uint32_t inter[QO_KMAX];
         /* decode_data over ids 0..k-1: src/fec_rs_fnt.h:204-234 */
         decode_apply(c, enc_ctx, data, inter);
         qo_fft(c->n, c->data_len, c->r, inter, c->k, codeword);
@@ -318,11 +318,11 @@ void qo_encode_blocks(const qo_codec* c, uint8_t* const* data,
     size_t words = block_bytes / 2, j;
     int k = c->k, n = c->n, i, first = c->sys ? k : 0;
     qo_ctx* ctx = NULL;
-    uint32_t in[1024];
+    uint32_t in[QO_KMAX];
     uint32_t* cw = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
 
     if (c->sys) {
-        uint32_t ids[1024];
+        uint32_t ids[QO_KMAX];
         ctx = (qo_ctx*)malloc(sizeof(qo_ctx));
         for (i = 0; i < k; i++)
             ids[i] = (uint32_t)i;
@@ -365,15 +365,15 @@ int qo_decode_blocks(const qo_codec* c, uint8_t* const* data,
                      size_t block_bytes)
 {
     int k = c->k, i, fi = 0, avail_data = 0;
-    uint32_t ids[1024] = {0};
-    const uint8_t* src[1024];
-    const uint32_t* marks[1024];
-    uint32_t nmarks[1024];
-    uint32_t* sorted[1024];
-    uint32_t pos[1024];
+    uint32_t ids[QO_KMAX] = {0};
+    const uint8_t* src[QO_KMAX];
+    const uint32_t* marks[QO_KMAX];
+    uint32_t nmarks[QO_KMAX];
+    uint32_t* sorted[QO_KMAX];
+    uint32_t pos[QO_KMAX];
     size_t words = block_bytes / 2, j;
     qo_ctx* ctx;
-    uint32_t in[1024], out[1024];
+    uint32_t in[QO_KMAX], out[QO_KMAX];
 
     if (c->sys) {
         for (i = 0; i < k; i++) {
@@ -459,7 +459,7 @@ void qo_nf4_encode_blocks(const qo_codec* c, int word_size,
 {
     const int g = word_size / 2, k = c->k, no = c->n_outputs;
     const size_t words = block_bytes / (size_t)word_size; /* fec_base.h:1083 */
-    uint32_t in[1024];
+    uint32_t in[QO_KMAX];
     uint32_t* cw = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)c->n);
     uint32_t* mask = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)no);
     size_t j;
@@ -515,11 +515,11 @@ int qo_nf4_decode_blocks(const qo_codec* c, int word_size,
 {
     const int g = word_size / 2, k = c->k;
     const size_t words = block_bytes / (size_t)word_size;
-    uint32_t ids[1024] = {0};
-    const uint8_t* src[1024];
-    uint64_t* marks[1024]; /* word << 8 | component mask, sorted */
-    uint32_t nmarks[1024], pos[1024], cur[1024];
-    uint32_t in[1024], out[1024];
+    uint32_t ids[QO_KMAX] = {0};
+    const uint8_t* src[QO_KMAX];
+    uint64_t* marks[QO_KMAX]; /* word << 8 | component mask, sorted */
+    uint32_t nmarks[QO_KMAX], pos[QO_KMAX], cur[QO_KMAX];
+    uint32_t in[QO_KMAX], out[QO_KMAX];
     int i, fi = 0, comp;
     size_t j, e;
     qo_ctx* ctx;
@@ -644,8 +644,8 @@ int qo_fnt32_encode(const qo_codec* c, uint8_t** data, uint8_t** parity,
 {
     int md = qo_metadata_size(block_size), nd = md / 4, i, k = c->k;
     uint32_t cap = (uint32_t)nd;
-    uint8_t* in[1024];
-    uint8_t* out[2048];
+    uint8_t* in[QO_KMAX];
+    uint8_t* out[QO_NMAX];
     uint32_t* oor = (uint32_t*)malloc(sizeof(uint32_t) * cap *
                                       (size_t)c->n_outputs);
     uint32_t* cnt = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)c->n_outputs);
@@ -727,9 +727,9 @@ int qo_fnt32_decode(const qo_codec* c, uint8_t** data, uint8_t** parity,
     uint32_t* oor = (uint32_t*)malloc(sizeof(uint32_t) * cap *
                                       (size_t)c->n_outputs);
     uint32_t* cnt = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)c->n_outputs);
-    uint8_t* dv[1024];
-    uint8_t* pv[2048];
-    int wanted[1024];
+    uint8_t* dv[QO_KMAX];
+    uint8_t* pv[QO_NMAX];
+    int wanted[QO_KMAX];
     int ret = 0;
 
     if (load_props(c, data, parity, missing_idxs, nd, oor, cnt, cap)) {
@@ -786,11 +786,11 @@ int qo_fnt32_reconstruct(const qo_codec* c, uint8_t** data, uint8_t** parity,
     uint32_t* eoor = (uint32_t*)malloc(sizeof(uint32_t) * cap *
                                        (size_t)c->n_outputs);
     uint32_t* ecnt = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)c->n_outputs);
-    uint8_t* dv[1024];
-    uint8_t* pv[2048];
-    uint8_t* ov[2048];
-    uint8_t* tmp[1024];
-    int wanted[1024];
+    uint8_t* dv[QO_KMAX];
+    uint8_t* pv[QO_NMAX];
+    uint8_t* ov[QO_NMAX];
+    uint8_t* tmp[QO_KMAX];
+    int wanted[QO_KMAX];
     int ret = 0, need_decode = 0;
 
     for (i = 0; i < k; i++)

@@ -24,6 +24,9 @@ extern "C" {
 #endif
 
 #define QO_Q 65537u
+/* oracle limits (fixed-size scratch): k <= QO_KMAX, k + m <= 65536 */
+#define QO_KMAX 4096
+#define QO_NMAX 65536
 
 /* ---- GF(65537) scalar arithmetic: src/gf_ring.h:214-286 ---- */
 uint32_t qo_add(uint32_t a, uint32_t b);
@@ -58,9 +61,9 @@ void qo_fft_inv(int n, uint32_t w, const uint32_t* in, uint32_t* out);
 /* Decode context for a set of k fragment ids (src/fec_context.h:66-274). */
 typedef struct {
     int k;
-    uint32_t ids[1024];
-    uint32_t inv_A_i[1024];
-    uint32_t A_fft_2k[2048];
+    uint32_t ids[QO_KMAX];
+    uint32_t inv_A_i[QO_KMAX];
+    uint32_t A_fft_2k[2 * QO_KMAX];
 } qo_ctx;
 
 int qo_ctx_init(const qo_codec* c, qo_ctx* ctx, const uint32_t* ids);

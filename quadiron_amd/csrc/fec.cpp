@@ -141,7 +141,7 @@ RsFnt::RsFnt(FecType t, unsigned ws, unsigned k, unsigned m, size_t pkt)
                            t == FecType::SYSTEMATIC ? 1 : 0);
     if (!plan_)
         throw std::runtime_error(
-            "RsFnt: cannot create the GPU plan (no HIP device or k > 128)");
+            "RsFnt: cannot create the GPU plan (no HIP device)");
     n = static_cast<unsigned>(qi_plan_n(plan_));
     const hipError_t e =
         hipStreamCreateWithFlags(&plan_->host.stream, hipStreamNonBlocking);
@@ -280,21 +280,16 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
     check(hipMemcpyAsync(h.ids.p, hids.data(), k * 2, hipMemcpyHostToDevice, s),
           "H2D");
     // received rows staged by position; OOR buckets by position
-    Oor in{reinterpret_cast<uint32_t*>(dcb + cnt_off),
-           reinterpret_cast<uint32_t*>(dcb + ent_off), k,
-           static_cast<int>(cap)};
-    check_rc(build_ctx(plan_, static_cast<uint16_t*>(h.ids.p), hids.data(), 1,
-                       &in, 0, 1, static_cast<long long>(words), h.ctx.p, s),
+    uint32_t* dcnt = reinterpret_cast<uint32_t*>(dcb + cnt_off);
+    uint32_t* dent = reinterpret_cast<uint32_t*>(dcb + ent_off);
+    check_rc(qi_gpu_decode_ctx_packed(plan_, static_cast<uint16_t*>(h.ids.p), hids.data(), 1,
+                                      dcnt, dent, static_cast<int>(cap),
+                                      static_cast<long long>(words), h.ctx.p, s),
              "decode context");
-    const MatLayout L{k, k, matrix_kp(k)};
-    RowSrc src{din, 0, static_cast<long long>(P), 1 << 30, nullptr, 0, 0, 1, k, 0};
-    RowDst dst{dout, 0, static_cast<long long>(P)};
-    const int32_t* ctx = static_cast<const int32_t*>(h.ctx.p);
-    check_rc(launch_matrix(L, ctx, 0, ctx + L.words(), 0, src, dst,
-                           static_cast<long long>(words), 1, &in, 0, nullptr,
-                           reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
-                           0, ctx_slow(plan_, h.ctx.p, static_cast<long long>(words)),
-                           plan_->d_err, s),
+    check_rc(qi_gpu_decode_packed(plan_, h.ctx.p, din, 0, static_cast<long long>(P), dcnt,
+                                  dent, static_cast<int>(cap), dout, 0,
+                                  static_cast<long long>(P), static_cast<long long>(words), 1,
+                                  s),
              "decode");
     for (int t = 0; t < k; t++)
         if (outputs[t])

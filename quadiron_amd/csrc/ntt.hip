@@ -1,0 +1,733 @@
+// General-k RS-FNT path (k > 64): NTT-structured encode and decode.
+//
+// Codes with k > 64 do not fit the register codelets of encode_fnt_kernel
+// (K = ceil2(k) <= 64) nor the k x k interpolation matrices of the matrix
+// kernels, and their O(k^2) per column would lose to the transforms anyway.
+// They run the reference's own algorithm as column-batched NTTs:
+//
+//   non-systematic encode  NTT_n of the k data rows zero-padded to n
+//                          (Radix2::fft, src/fft_2n.h:360-407; outputs
+//                          0 .. k+m-1, src/fec_rs_fnt.h:236-251)
+//   decode                 FecCode::decode_apply (src/fec_base.h:1418-1448):
+//                            y_i = v_i * inv_A_i      (65536 restored at the
+//                                                      OOR marks first,
+//                                                      decode_prepare :1361-1404)
+//                            INTT_n of the y_i placed at positions z_i = ids
+//                            NTT_2k of its first k outputs (zero-extended)
+//                            x C[j] = -A_fft_2k[j] / len_2k
+//                            INTT_2k; first k outputs = the coefficients
+//                          (ifft's 1/N and the final negation are folded into
+//                          the per-pattern constants C: linear maps commute)
+//   systematic decode      the same, then NTT_n evaluated at r^t, t < k
+//                          (src/fec_base.h:1348-1353)
+//   systematic encode      the interpolation through the data at r^0..r^{k-1}
+//                          (the plan's constant context), then NTT_n, outputs
+//                          k .. k+m-1 (src/fec_rs_fnt.h:236-251)
+//
+// Transforms.  X[u] = sum_t x[t] w^(+-ut) down the rows of every column,
+// N = 2^b <= 65536, as in-place decimation-in-time passes of radix R <= 32
+// over an int32 HBM scratch: pass p (stride S = prod_{q<p} R_q) takes the R
+// positions b + s + j S of a group, multiplies element j by w_{SR}^{s j}
+// (a wave-uniform table entry) and applies an R-point register codelet
+// (fnt_codelets.h, interval-planned lazy reduction).  Pass 0 gathers its
+// input in digit-reversed order straight from the source rows (zero past the
+// source's rows: the pruned input of Radix2::fft's replicated shortcut,
+// src/fft_2n.h:360-407); the last pass writes canonical u16 rows (and OOR
+// marks) or leaves the result in the scratch.  Lanes are columns: every load
+// and store is a coalesced row run.  The inverse transform uses the same
+// codelets with the output index reversed (DFT(x)[-u] = IDFT(x)[u]) and the
+// inverse twiddle table.
+//
+// The per-pattern context (DecodeContext::init, src/fec_context.h:232-274:
+// A(x) = prod (x - x_i), 1/(x_i A'(x_i)), FFT_2k(A)) is built on the GPU, one
+// workgroup per stripe, inside the caller's stream (no host round trip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "fnt_codelets.h"
+#include "gf65537.h"
+#include "qi_internal.h"
+#include "qi_plan.h"
+
+namespace qi {
+
+namespace {
+
+constexpr int kNttBlock = 256;
+constexpr int kMaxPasses = 16;
+
+// x * c mod q for |x| < 2^23 and a balanced twiddle |c| <= 32768: the full
+// 48-bit product as v_mul_i32_i24 + v_mul_hi_i32_i24, reduced with
+// 2^32 = 1 and 2^16 = -1 (p = hi 2^32 + lo: lo16 - hi16 + hi).  Result in
+// [-65536, 65535].
+__device__ __forceinline__ int32_t mul_rt(int32_t x, int32_t c)
+{
+    const long long p = static_cast<long long>(sext24(x)) * static_cast<long long>(sext24(c));
+    const uint32_t lo = static_cast<uint32_t>(p);
+    const int32_t hi = static_cast<int32_t>(p >> 32);
+    return static_cast<int32_t>(lo & 0xffffu) - static_cast<int32_t>(lo >> 16) + hi;
+}
+
+// canonical residue of a V-range value [-2, 65537]
+__device__ __forceinline__ uint32_t canon_vr(int32_t y)
+{
+    const int32_t c = y < 0 ? y + 65537 : y;
+    return static_cast<uint32_t>(c >= 65537 ? c - 65537 : c);
+}
+
+// codelet input range: gathered u16 (or restored 65536), scratch values
+// (V range) and twiddled values [-65536, 65535]
+constexpr long long kInLo = -65540, kInHi = 65540;
+
+}  // namespace
+
+// One pass of a transform (all parameters uniform).  Every per-stripe
+// pointer is already offset to the first stripe of the launch and to the
+// first column of the slice.
+struct NttPassArgs {
+    int N, S, R, twstep;  // length, stride, radix of this pass; table step
+    int first, last, inverse, npass;
+    int radix[kMaxPasses];  // the whole radix list (pass 0's digit reversal)
+    const int32_t* tw;      // balanced w_nmax^e (inverse table: w_nmax^-e)
+    int32_t* scr;           // position P of stripe s at scr + s*sss + P*cols
+    long long sss, cols;
+    // pass 0 source: sequence element t is source row row(t) = posmap[t]
+    // (or t) at in + s*iss + row*irs, u16 or int32; rows outside
+    // [0, in_rows) read as zero; optional multiplier scale[s*scs + t]
+    const void* in;
+    long long iss, irs;
+    int in_u16, in_rows;
+    const int32_t* posmap;
+    const int32_t* scale;
+    long long pms, scs;
+    // last pass: positions row0 .. row0+out_rows-1 -> u16 rows of out (or
+    // stay in the scratch when out is null); OOR marks with absolute column
+    // col0 + c into buckets slot = row
+    uint16_t* out;
+    long long oss, ors;
+    int row0, out_rows;
+    long long col0;
+    Oor oor;
+    int tiles;  // column tiles of kNttBlock
+};
+
+template <int R>
+__global__ __launch_bounds__(kNttBlock) void ntt_pass_kernel(NttPassArgs a)
+{
+    const int tiles = a.tiles;
+    const int s = blockIdx.x / tiles;
+    const int tile = blockIdx.x - s * tiles;
+    const long long c = static_cast<long long>(tile) * kNttBlock + threadIdx.x;
+    if (c >= a.cols)
+        return;
+    const int grp = blockIdx.y;
+    const int S = a.S, N = a.N;
+    const int ss = grp % S;             // offset inside the group, [0, S)
+    const int b = (grp / S) * (S * R);  // group start
+    int32_t* scr = a.scr + s * a.sss;
+    int32_t v[R];
+    if (a.first) {
+        // digit-reversed gather: position b + j holds x[t_rest(b) + j N/R0]
+        int trest = 0, Sp = R;
+        for (int p = 1; p < a.npass; p++) {
+            const int Rp = a.radix[p];
+            trest += ((b / Sp) % Rp) * (N / (Sp * Rp));
+            Sp *= Rp;
+        }
+        const int step = N / R;
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            const int t = trest + j * step;
+            const int row = a.posmap ? a.posmap[s * a.pms + t] : t;
+            int32_t x = 0;
+            if (row >= 0 && row < a.in_rows) {  // uniform
+                if (a.in_u16)
+                    x = static_cast<const uint16_t*>(a.in)[s * a.iss + row * a.irs + c];
+                else
+                    x = static_cast<const int32_t*>(a.in)[s * a.iss + row * a.irs + c];
+                if (a.scale)
+                    x = mul_rt(x, a.scale[s * a.scs + t]);
+            }
+            v[j] = x;
+        }
+    } else {
+        const int tstep = N / (S * R);
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            int32_t x = scr[static_cast<long long>(b + ss + j * S) * a.cols + c];
+            if (j > 0 && ss > 0)  // w_{SR}^{ss j} = w_N^{ss j N/(SR)}
+                x = mul_rt(x, a.tw[ss * j * tstep * a.twstep]);
+            v[j] = x;
+        }
+    }
+    dft<R, kInLo, kInHi>(v);  // natural order, outputs in V = [-2, 65537]
+    if (a.last && a.out) {
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            const int32_t y = v[a.inverse ? (R - u) % R : u];
+            const int row = b + ss + u * S - a.row0;
+            if (row >= 0 && row < a.out_rows) {  // uniform
+                const uint32_t cv = canon_vr(y);
+                a.out[s * a.oss + row * a.ors + c] = static_cast<uint16_t>(cv);
+                if (cv == 65536u && a.oor.counts) {
+                    const long long bk = static_cast<long long>(s) * a.oor.slots + row;
+                    const uint32_t e = atomicAdd(&a.oor.counts[bk], 1u);
+                    if (e < static_cast<uint32_t>(a.oor.cap))
+                        a.oor.entries[bk * a.oor.cap + e] = static_cast<uint32_t>(a.col0 + c);
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < R; u++)
+            scr[static_cast<long long>(b + ss + u * S) * a.cols + c] =
+                v[a.inverse ? (R - u) % R : u];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-pattern decode context (DecodeContext::init, src/fec_context.h:232-274)
+// ctx per stripe (int32): inv_A_i[k] | C[len_2k] | posmap[n] | ids[k]
+// ---------------------------------------------------------------------------
+struct NttCtxLayout {
+    int k, n, len2k;
+    __host__ __device__ long long c_off() const { return k; }
+    __host__ __device__ long long pos_off() const { return static_cast<long long>(k) + len2k; }
+    __host__ __device__ long long ids_off() const { return pos_off() + n; }
+    __host__ __device__ long long words() const { return ids_off() + k; }
+};
+
+__device__ __forceinline__ uint32_t mulm_(uint32_t a, uint32_t b)
+{
+    const uint64_t p = static_cast<uint64_t>(a) * b;
+    const int32_t v = static_cast<int32_t>(p & 0xffffu) -
+                      static_cast<int32_t>((p >> 16) & 0xffffu) + static_cast<int32_t>(p >> 32);
+    return static_cast<uint32_t>(v < 0 ? v + 65537 : v);
+}
+__device__ __forceinline__ uint32_t addm_(uint32_t a, uint32_t b)
+{
+    const uint32_t c = a + b;
+    return c >= 65537u ? c - 65537u : c;
+}
+__device__ __forceinline__ uint32_t subm_(uint32_t a, uint32_t b)
+{
+    return a >= b ? a - b : a + 65537u - b;
+}
+__device__ __forceinline__ uint32_t powm_(uint32_t b, uint32_t e)
+{
+    uint32_t r = 1;
+    for (; e; e >>= 1) {
+        if (e & 1)
+            r = mulm_(r, b);
+        b = mulm_(b, b);
+    }
+    return r;
+}
+
+struct NttCtxArgs {
+    NttCtxLayout L;
+    uint32_t r, w2k;      // n-th and len_2k-th roots of unity
+    uint32_t inv_len2k;   // len_2k^-1
+    const uint16_t* ids;  // S x k fragment ids (nullptr: 0 .. k-1)
+    int32_t* ctx;
+    long long cs;
+};
+
+__global__ __launch_bounds__(kNttBlock) void ntt_ctx_kernel(NttCtxArgs a)
+{
+    extern __shared__ uint32_t A[];  // k + 1 coefficients of A(x)
+    const int s = blockIdx.x, tid = threadIdx.x, k = a.L.k;
+    int32_t* ctx = a.ctx + s * a.cs;
+    int32_t* invA = ctx;
+    int32_t* C = ctx + a.L.c_off();
+    int32_t* posmap = ctx + a.L.pos_off();
+    int32_t* ids = ctx + a.L.ids_off();
+    for (int i = tid; i < k; i += kNttBlock) {
+        const int id = a.ids ? a.ids[static_cast<long long>(s) * k + i] : i;
+        ids[i] = id;
+        invA[i] = static_cast<int32_t>(powm_(a.r, static_cast<uint32_t>(id)));  // x_i for now
+    }
+    for (int d = tid; d <= k; d += kNttBlock)
+        A[d] = d == 0 ? 1u : 0u;
+    for (int t = tid; t < a.L.n; t += kNttBlock)
+        posmap[t] = -1;
+    __syncthreads();
+    // A(x) = prod_i (x - x_i)  (Poly::mul_to_x_plus_coef, src/vec_poly.h):
+    // A <- A (x - x_i) in place, each thread on a contiguous chunk of
+    // coefficients from the top down, the chunk's lower neighbour value
+    // saved before the update
+    const int chunk = (k + 1 + kNttBlock - 1) / kNttBlock;
+    const int lo = tid * chunk, hi = min(lo + chunk, k + 1);
+    for (int i = 0; i < k; i++) {
+        const uint32_t xi = static_cast<uint32_t>(invA[i]);
+        const int top = min(hi - 1, i + 1);
+        const uint32_t below = (lo >= 1 && lo <= top) ? A[lo - 1] : 0u;
+        __syncthreads();
+        for (int d = top; d >= lo; d--) {
+            const uint32_t lowr = d == 0 ? 0u : (d - 1 >= lo ? A[d - 1] : below);
+            A[d] = subm_(lowr, mulm_(xi, A[d]));
+        }
+        __syncthreads();
+    }
+    // 1 / (x_i A'(x_i)): A' by Horner on d A[d]
+    for (int i = tid; i < k; i += kNttBlock) {
+        const uint32_t xi = static_cast<uint32_t>(invA[i]);
+        uint32_t acc = 0;
+        for (int d = k; d >= 1; d--)
+            acc = addm_(mulm_(acc, xi), mulm_(A[d], static_cast<uint32_t>(d)));
+        invA[i] = static_cast<int32_t>(powm_(mulm_(acc, xi), 65535u));
+        posmap[ids[i]] = i;
+    }
+    // C[j] = -A(w2k^j) / len_2k  (FFT_2k(A) with ifft's scale and the final
+    // negation of decode_apply folded in)
+    for (int j = tid; j < a.L.len2k; j += kNttBlock) {
+        const uint32_t xj = powm_(a.w2k, static_cast<uint32_t>(j));
+        uint32_t acc = 0;
+        for (int d = k; d >= 0; d--)
+            acc = addm_(mulm_(acc, xj), A[d]);
+        C[j] = static_cast<int32_t>(subm_(0u, mulm_(acc, a.inv_len2k)));
+    }
+}
+
+// decode step 1: received row i of stripe s -> scratch row i, y = v inv_A_i
+struct NttExpandArgs {
+    RowSrc src;  // offset to the slice's first column and stripe
+    const int32_t* ctx;
+    long long cs;
+    int ids_off, k;
+    int32_t* scr;
+    long long sss, cols;
+    int tiles;
+};
+
+__global__ __launch_bounds__(kNttBlock) void ntt_expand_kernel(NttExpandArgs a)
+{
+    const int tiles = a.tiles;
+    const int s = blockIdx.x / tiles;
+    const int tile = blockIdx.x - s * tiles;
+    const int i = blockIdx.y;
+    const long long c = static_cast<long long>(tile) * kNttBlock + threadIdx.x;
+    if (c >= a.cols)
+        return;
+    const int32_t* ctx = a.ctx + s * a.cs;
+    const int id = a.src.by_pos ? i : ctx[a.ids_off + i];
+    const uint16_t* row = id < a.src.split
+                              ? a.src.base0 + s * a.src.ss0 + id * a.src.rs0
+                              : a.src.base1 + s * a.src.ss1 + (id - a.src.split) * a.src.rs1;
+    const int32_t x = row[c];
+    a.scr[s * a.sss + static_cast<long long>(i) * a.cols + c] =
+        mul_rt(x, balanced(static_cast<uint32_t>(ctx[i])));
+}
+
+// decode step 1b (decode_prepare, src/fec_base.h:1361-1404): a marked symbol
+// is 65536 = -1 whatever was stored, so y = -inv_A_i at the marks of the
+// slice [c0, c0 + cols).  One workgroup per (stripe, received row).
+struct NttFixArgs {
+    Oor in;  // offset to the launch's first stripe
+    int slot_base, by_pos;
+    const int32_t* ctx;
+    long long cs;
+    int ids_off;
+    int32_t* scr;
+    long long sss, cols, c0;
+    uint32_t* err;
+};
+
+__global__ __launch_bounds__(kNttBlock) void ntt_fix_kernel(NttFixArgs a)
+{
+    const int s = blockIdx.x, i = blockIdx.y;
+    const int32_t* ctx = a.ctx + s * a.cs;
+    const int slot = a.by_pos ? i : ctx[a.ids_off + i] - a.slot_base;
+    if (slot < 0)
+        return;  // systematic data row: no marks
+    const long long bk = static_cast<long long>(s) * a.in.slots + slot;
+    uint32_t cnt = a.in.counts[bk];
+    if (cnt > static_cast<uint32_t>(a.in.cap)) {
+        if (threadIdx.x == 0)
+            atomicOr(a.err, kErrOorTruncated);
+        cnt = static_cast<uint32_t>(a.in.cap);
+    }
+    const int32_t y = 65537 - static_cast<int32_t>(ctx[i]);  // -inv_A_i in [1, 65537]
+    for (uint32_t e = threadIdx.x; e < cnt; e += kNttBlock) {
+        const long long col = static_cast<long long>(a.in.entries[bk * a.in.cap + e]) - a.c0;
+        if (col >= 0 && col < a.cols)
+            a.scr[s * a.sss + static_cast<long long>(i) * a.cols + col] = y;
+    }
+}
+
+namespace {
+
+int ilog2i(long long v)
+{
+    int l = 0;
+    while ((1LL << l) < v)
+        l++;
+    return l;
+}
+
+// radices <= 32, as even as possible
+std::vector<int> radices(int N)
+{
+    const int bits = ilog2i(N);
+    const int m = std::max(1, (bits + 4) / 5);
+    std::vector<int> r;
+    int left = bits;
+    for (int p = 0; p < m; p++) {
+        const int bp = (left + (m - p) - 1) / (m - p);
+        r.push_back(1 << bp);
+        left -= bp;
+    }
+    return r;
+}
+
+int launch_pass(const NttPassArgs& a, int S, hipStream_t st)
+{
+    const dim3 grid(static_cast<unsigned>(a.tiles) * static_cast<unsigned>(S),
+                    static_cast<unsigned>(a.N / a.R));
+    switch (a.R) {
+#define QI_NTT_R(RR)                                                              \
+    case RR:                                                                      \
+        hipLaunchKernelGGL(ntt_pass_kernel<RR>, grid, dim3(kNttBlock), 0, st, a); \
+        break;
+        QI_NTT_R(2)
+        QI_NTT_R(4)
+        QI_NTT_R(8)
+        QI_NTT_R(16)
+        QI_NTT_R(32)
+#undef QI_NTT_R
+    default:
+        return -3;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// One transform of length N over S stripes: pass 0 gathers from a.in, the
+// last pass writes a.out rows (or leaves the result in a.scr).
+int transform(NttPassArgs a, const qi_plan* p, int N, bool inverse, int S, hipStream_t st)
+{
+    const std::vector<int> rs = radices(N);
+    if (N < 2 || N > p->nmax || static_cast<int>(rs.size()) > kMaxPasses)
+        return -3;
+    a.N = N;
+    a.inverse = inverse ? 1 : 0;
+    a.tw = p->d_tw[inverse ? 1 : 0];
+    a.twstep = p->nmax / N;
+    a.npass = static_cast<int>(rs.size());
+    for (int q = 0; q < a.npass; q++)
+        a.radix[q] = rs[q];
+    int Sp = 1;
+    uint16_t* out = a.out;
+    for (int q = 0; q < a.npass; q++) {
+        a.R = rs[q];
+        a.S = Sp;
+        a.first = q == 0;
+        a.last = q == a.npass - 1;
+        a.out = a.last ? out : nullptr;
+        if (const int rc = launch_pass(a, S, st))
+            return rc;
+        Sp *= rs[q];
+    }
+    return 0;
+}
+
+// slice geometry: columns per slice and stripes per launch so that one
+// scratch buffer (nmax rows x cols int32 per stripe) stays within ~256 MiB
+struct Slicing {
+    long long W;
+    int Sg;
+};
+
+Slicing slicing(const qi_plan* p, long long words, int S)
+{
+    const long long budget = 64LL << 20;  // int32 elements per buffer
+    const long long wp = (words + kNttBlock - 1) / kNttBlock * kNttBlock;
+    long long W = budget / p->nmax / kNttBlock * kNttBlock;
+    W = std::max<long long>(kNttBlock, std::min(W, wp));
+    const long long sg = std::max<long long>(1, budget / (p->nmax * W));
+    return Slicing{W, static_cast<int>(std::min<long long>(sg, S))};
+}
+
+struct Scratch {
+    void* p = nullptr;
+    hipStream_t st = nullptr;
+    ~Scratch()
+    {
+        if (p)
+            (void)hipFreeAsync(p, st);
+    }
+};
+
+NttCtxLayout ctx_layout_of(const qi_plan* p)
+{
+    return NttCtxLayout{p->k, p->n, p->len2k};
+}
+
+RowSrc offset_src(RowSrc s, int sg0, long long c0)
+{
+    s.base0 += sg0 * s.ss0 + c0;
+    if (s.base1)
+        s.base1 += sg0 * s.ss1 + c0;
+    return s;
+}
+
+// The interpolation (decode_apply) of Sg stripes over the slice: the k
+// received rows -> coefficient rows.  res != null: the k coefficient rows
+// are written there as u16; otherwise they stay in scratch B (int32).
+int interpolate(const qi_plan* p, const int32_t* ctx, long long cs, const RowSrc& src,
+                const Oor* in_oor, int slot_base, long long c0, long long cols, int Sg,
+                int32_t* A, int32_t* B, long long sss, const RowDst* res, uint32_t* err,
+                hipStream_t st)
+{
+    const NttCtxLayout L = ctx_layout_of(p);
+    const int tiles = static_cast<int>((cols + kNttBlock - 1) / kNttBlock);
+    // y_i = v_i inv_A_i -> A rows 0..k-1
+    NttExpandArgs e{src, ctx, cs, static_cast<int>(L.ids_off()), p->k, A, sss, cols, tiles};
+    hipLaunchKernelGGL(ntt_expand_kernel, dim3(tiles * Sg, p->k), dim3(kNttBlock), 0, st, e);
+    if (hipGetLastError() != hipSuccess)
+        return -2;
+    if (in_oor && in_oor->counts) {
+        NttFixArgs f{*in_oor, slot_base, src.by_pos, ctx, cs, static_cast<int>(L.ids_off()),
+                     A, sss, cols, c0, err};
+        hipLaunchKernelGGL(ntt_fix_kernel, dim3(Sg, p->k), dim3(kNttBlock), 0, st, f);
+        if (hipGetLastError() != hipSuccess)
+            return -2;
+    }
+    NttPassArgs a{};
+    a.tiles = tiles;
+    a.cols = cols;
+    a.sss = sss;
+    // INTT_n of the y_i placed at positions z_i (buf1_n) -> B
+    a.scr = B;
+    a.in = A;
+    a.iss = sss;
+    a.irs = cols;
+    a.in_u16 = 0;
+    a.in_rows = p->k;
+    a.posmap = ctx + L.pos_off();
+    a.pms = cs;
+    if (int rc = transform(a, p, p->n, true, Sg, st))
+        return rc;
+    // NTT_2k of its first k outputs (zero-extended) -> A
+    a.scr = A;
+    a.in = B;
+    a.posmap = nullptr;
+    if (int rc = transform(a, p, p->len2k, false, Sg, st))
+        return rc;
+    // x C, INTT_2k -> the k coefficient rows (res, or B)
+    a.scr = B;
+    a.in = A;
+    a.in_rows = p->len2k;
+    a.scale = ctx + L.c_off();
+    a.scs = cs;
+    if (res) {
+        a.out = res->base;
+        a.oss = res->ss;
+        a.ors = res->rs;
+        a.row0 = 0;
+        a.out_rows = p->k;
+    }
+    return transform(a, p, p->len2k, true, Sg, st);
+}
+
+}  // namespace
+
+long long ntt_ctx_words(const qi_plan* p)
+{
+    return ctx_layout_of(p).words();
+}
+
+int ntt_build_ctx(const qi_plan* p, const uint16_t* d_ids, int S, int32_t* ctx, long long cs,
+                  hipStream_t st)
+{
+    if (S <= 0)
+        return 0;
+    NttCtxArgs a{ctx_layout_of(p), p->r, root_of_unity(static_cast<uint32_t>(p->len2k)),
+                 invmod_c(static_cast<uint32_t>(p->len2k)), d_ids, ctx, cs};
+    const size_t lds = static_cast<size_t>(p->k + 1) * 4;
+    if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_ctx_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           static_cast<int>(lds)) != hipSuccess)
+        return -2;
+    hipLaunchKernelGGL(ntt_ctx_kernel, dim3(S), dim3(kNttBlock), lds, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int ntt_plan_init(qi_plan* p)
+{
+    p->len2k = static_cast<int>(ceil2(static_cast<uint32_t>(2 * p->k)));
+    p->nmax = std::max(p->n, p->len2k);
+    if (p->nmax > 65536)
+        return -1;
+    const uint32_t w = root_of_unity(static_cast<uint32_t>(p->nmax));
+    const uint32_t wi = invmod_c(w);
+    std::vector<int32_t> tw(2 * static_cast<size_t>(p->nmax));
+    uint32_t f = 1, g = 1;
+    for (int e = 0; e < p->nmax; e++) {
+        tw[e] = balanced(f);
+        tw[p->nmax + e] = balanced(g);
+        f = mulmod_c(f, w);
+        g = mulmod_c(g, wi);
+    }
+    int32_t* d = nullptr;
+    if (hipMalloc(&d, tw.size() * 4) != hipSuccess)
+        return -2;
+    p->d_tw[0] = d;
+    p->d_tw[1] = d + p->nmax;
+    if (hipMemcpy(d, tw.data(), tw.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return -2;
+    if (p->sys) {
+        // the systematic encode's constant context: points r^0 .. r^{k-1}
+        const long long cs = ntt_ctx_words(p);
+        if (hipMalloc(&p->d_sysctx, cs * 4) != hipSuccess)
+            return -2;
+        if (ntt_build_ctx(p, nullptr, 1, p->d_sysctx, cs, nullptr) ||
+            hipStreamSynchronize(nullptr) != hipSuccess)
+            return -2;
+    }
+    return 0;
+}
+
+void ntt_plan_free(qi_plan* p)
+{
+    if (p->d_tw[0])
+        (void)hipFree(p->d_tw[0]);
+    if (p->d_sysctx)
+        (void)hipFree(p->d_sysctx);
+    p->d_tw[0] = p->d_tw[1] = nullptr;
+    p->d_sysctx = nullptr;
+}
+
+// non-systematic: outputs 0 .. n_out-1 of NTT_n(data zero-padded);
+// systematic: parities k .. k+m-1 of NTT_n(interpolation of the data rows)
+int ntt_encode(const qi_plan* p, const uint16_t* data, long long dss, long long drs,
+               RowDst out, long long words, int S, const Oor* oor, hipStream_t st)
+{
+    if (S <= 0 || words <= 0)
+        return 0;
+    const Slicing sl = slicing(p, words, S);
+    const long long sss = static_cast<long long>(p->nmax) * sl.W;
+    Scratch sa, sb;
+    sa.st = sb.st = st;
+    const size_t bytes = static_cast<size_t>(sl.Sg) * sss * 4;
+    if (hipMallocAsync(&sa.p, bytes, st) != hipSuccess ||
+        (p->sys && hipMallocAsync(&sb.p, bytes, st) != hipSuccess))
+        return -2;
+    int32_t* A = static_cast<int32_t*>(sa.p);
+    int32_t* B = static_cast<int32_t*>(sb.p);
+    for (int sg0 = 0; sg0 < S; sg0 += sl.Sg) {
+        const int Sg = std::min(sl.Sg, S - sg0);
+        for (long long c0 = 0; c0 < words; c0 += sl.W) {
+            const long long cols = std::min(sl.W, words - c0);
+            NttPassArgs a{};
+            a.tiles = static_cast<int>((cols + kNttBlock - 1) / kNttBlock);
+            a.cols = cols;
+            a.sss = sss;
+            a.out = out.base + sg0 * out.ss + c0;
+            a.oss = out.ss;
+            a.ors = out.rs;
+            a.out_rows = p->n_outputs;
+            a.col0 = c0;
+            if (oor && oor->counts) {
+                a.oor = *oor;
+                a.oor.counts += static_cast<long long>(sg0) * oor->slots;
+                a.oor.entries += static_cast<long long>(sg0) * oor->slots * oor->cap;
+            }
+            const uint16_t* din = data + sg0 * dss + c0;
+            if (!p->sys) {
+                a.scr = A;
+                a.in = din;
+                a.iss = dss;
+                a.irs = drs;
+                a.in_u16 = 1;
+                a.in_rows = p->k;
+                a.row0 = 0;
+                if (int rc = transform(a, p, p->n, false, Sg, st))
+                    return rc;
+            } else {
+                const RowSrc src{din, dss, drs, 1 << 30, nullptr, 0, 0, 1, p->k, 0};
+                if (int rc = interpolate(p, p->d_sysctx, 0, src, nullptr, 0, c0, cols, Sg, A, B,
+                                         sss, nullptr, p->d_err, st))
+                    return rc;
+                // coefficient rows (B) -> NTT_n -> rows k .. k+m-1
+                a.scr = A;
+                a.in = B;
+                a.iss = sss;
+                a.irs = cols;
+                a.in_u16 = 0;
+                a.in_rows = p->k;
+                a.row0 = p->k;
+                if (int rc = transform(a, p, p->n, false, Sg, st))
+                    return rc;
+            }
+        }
+    }
+    return 0;
+}
+
+// decode of S stripes: ctx from ntt_build_ctx; src as in launch_matrix (by
+// id through the context's ids, or by position); in_oor buckets by slot =
+// id - slot_base (or position)
+int ntt_decode(const qi_plan* p, const int32_t* ctx, long long cs, RowSrc src,
+               const Oor* in_oor, int slot_base, RowDst out, long long words, int S,
+               hipStream_t st)
+{
+    if (S <= 0 || words <= 0)
+        return 0;
+    const Slicing sl = slicing(p, words, S);
+    const long long sss = static_cast<long long>(p->nmax) * sl.W;
+    Scratch sa, sb;
+    sa.st = sb.st = st;
+    const size_t bytes = static_cast<size_t>(sl.Sg) * sss * 4;
+    if (hipMallocAsync(&sa.p, bytes, st) != hipSuccess ||
+        hipMallocAsync(&sb.p, bytes, st) != hipSuccess)
+        return -2;
+    int32_t* A = static_cast<int32_t*>(sa.p);
+    int32_t* B = static_cast<int32_t*>(sb.p);
+    for (int sg0 = 0; sg0 < S; sg0 += sl.Sg) {
+        const int Sg = std::min(sl.Sg, S - sg0);
+        const int32_t* cx = ctx + sg0 * cs;
+        Oor io{};
+        if (in_oor && in_oor->counts) {
+            io = *in_oor;
+            io.counts += static_cast<long long>(sg0) * in_oor->slots;
+            io.entries += static_cast<long long>(sg0) * in_oor->slots * in_oor->cap;
+        }
+        for (long long c0 = 0; c0 < words; c0 += sl.W) {
+            const long long cols = std::min(sl.W, words - c0);
+            const RowSrc s2 = offset_src(src, sg0, c0);
+            RowDst o{out.base + sg0 * out.ss + c0, out.ss, out.rs};
+            if (!p->sys) {
+                if (int rc = interpolate(p, cx, cs, s2, io.counts ? &io : nullptr, slot_base, c0,
+                                         cols, Sg, A, B, sss, &o, p->d_err, st))
+                    return rc;
+                continue;
+            }
+            if (int rc = interpolate(p, cx, cs, s2, io.counts ? &io : nullptr, slot_base, c0,
+                                     cols, Sg, A, B, sss, nullptr, p->d_err, st))
+                return rc;
+            // the data rows are the evaluations at r^t, t < k
+            NttPassArgs a{};
+            a.tiles = static_cast<int>((cols + kNttBlock - 1) / kNttBlock);
+            a.cols = cols;
+            a.sss = sss;
+            a.scr = A;
+            a.in = B;
+            a.iss = sss;
+            a.irs = cols;
+            a.in_u16 = 0;
+            a.in_rows = p->k;
+            a.out = o.base;
+            a.oss = o.ss;
+            a.ors = o.rs;
+            a.row0 = 0;
+            a.out_rows = p->k;
+            if (int rc = transform(a, p, p->n, false, Sg, st))
+                return rc;
+        }
+    }
+    return 0;
+}
+
+}  // namespace qi

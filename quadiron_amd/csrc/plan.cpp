@@ -114,52 +114,54 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
     p->r = root_of_unity(static_cast<uint32_t>(p->n));
     (void)hipGetDevice(&p->device);
 
-    bool ok = true;
-    // twist factors w^{v t} for the encode passes (K <= 64)
-    if (!p->sys && p->K <= 64) {
-        const int passes = p->n / p->K;
-        std::vector<int32_t> tw(static_cast<size_t>(passes) * p->K);
-        for (int v = 0; v < passes; v++)
-            for (int t = 0; t < p->K; t++)
-                tw[static_cast<size_t>(v) * p->K + t] = balanced(powmod_c(
-                    p->r, static_cast<uint32_t>((static_cast<long long>(v) * t) % p->n)));
-        ok = ok && hipMalloc(&p->d_twist, tw.size() * 4) == hipSuccess &&
-             hipMemcpy(p->d_twist, tw.data(), tw.size() * 4,
-                       hipMemcpyHostToDevice) == hipSuccess;
-    }
-    // generator matrix for the systematic encode or for a non-systematic
-    // encode too wide for the register codelets: outputs x inputs
-    const int kp = matrix_kp(k);
-    if (kp < 0) {
-        ok = false;  // k > 64 is not supported by the matrix kernel
-    } else if (p->sys || p->K > 64 || enc_matrix_forced()) {
-        MatLayout L{p->n_outputs, k, kp};
-        std::vector<uint32_t> M;
-        if (p->sys) {
-            std::vector<uint32_t> ids(k), ev(m);
-            for (int i = 0; i < k; i++)
-                ids[i] = static_cast<uint32_t>(i);
-            for (int i = 0; i < m; i++)
-                ev[i] = powmod_c(p->r, static_cast<uint32_t>(k + i));
-            // parity i = P(r^{k+i}) where P interpolates data at r^0..r^{k-1}
-            // (src/fec_rs_fnt.h:204-251 SYSTEMATIC branch)
-            M = lagrange_matrix(k, p->r, ids.data(), 1, ev.data(), m);
-        } else {
-            M.resize(static_cast<size_t>(p->n_outputs) * k);
-            for (int i = 0; i < p->n_outputs; i++)
-                for (int t = 0; t < k; t++)
-                    M[static_cast<size_t>(i) * k + t] = powmod_c(
-                        p->r, static_cast<uint32_t>((static_cast<long long>(i) * t) % p->n));
+    bool ok = hipMalloc(&p->d_err, 4) == hipSuccess && hipMemset(p->d_err, 0, 4) == hipSuccess;
+    if (ok && p->K > 64) {
+        // k > 64: NTT-structured encode/decode (ntt.hip), any k + m <= 65536
+        p->ntt = 1;
+        ok = ntt_plan_init(p) == 0;
+    } else if (ok) {
+        // twist factors w^{v t} for the encode passes (K <= 64)
+        if (!p->sys && !enc_matrix_forced()) {
+            const int passes = p->n / p->K;
+            std::vector<int32_t> tw(static_cast<size_t>(passes) * p->K);
+            for (int v = 0; v < passes; v++)
+                for (int t = 0; t < p->K; t++)
+                    tw[static_cast<size_t>(v) * p->K + t] = balanced(powmod_c(
+                        p->r, static_cast<uint32_t>((static_cast<long long>(v) * t) % p->n)));
+            ok = hipMalloc(&p->d_twist, tw.size() * 4) == hipSuccess &&
+                 hipMemcpy(p->d_twist, tw.data(), tw.size() * 4, hipMemcpyHostToDevice) ==
+                     hipSuccess;
         }
-        std::vector<int32_t> blk(L.words());
-        pack_matrix(L, M.data(), blk.data());
-        p->gen = L;
-        ok = ok && hipMalloc(&p->d_gen, blk.size() * 4) == hipSuccess &&
-             hipMemcpy(p->d_gen, blk.data(), blk.size() * 4,
-                       hipMemcpyHostToDevice) == hipSuccess;
+        // generator matrix for the systematic encode (and the matrix-core
+        // A/B knob of the non-systematic one): outputs x inputs
+        if (ok && (p->sys || enc_matrix_forced())) {
+            const int kp = matrix_kp(k);
+            MatLayout L{p->n_outputs, k, kp};
+            std::vector<uint32_t> M;
+            if (p->sys) {
+                std::vector<uint32_t> ids(k), ev(m);
+                for (int i = 0; i < k; i++)
+                    ids[i] = static_cast<uint32_t>(i);
+                for (int i = 0; i < m; i++)
+                    ev[i] = powmod_c(p->r, static_cast<uint32_t>(k + i));
+                // parity i = P(r^{k+i}) where P interpolates data at r^0..r^{k-1}
+                // (src/fec_rs_fnt.h:204-251 SYSTEMATIC branch)
+                M = lagrange_matrix(k, p->r, ids.data(), 1, ev.data(), m);
+            } else {
+                M.resize(static_cast<size_t>(p->n_outputs) * k);
+                for (int i = 0; i < p->n_outputs; i++)
+                    for (int t = 0; t < k; t++)
+                        M[static_cast<size_t>(i) * k + t] = powmod_c(
+                            p->r, static_cast<uint32_t>((static_cast<long long>(i) * t) % p->n));
+            }
+            std::vector<int32_t> blk(L.words());
+            pack_matrix(L, M.data(), blk.data());
+            p->gen = L;
+            ok = hipMalloc(&p->d_gen, blk.size() * 4) == hipSuccess &&
+                 hipMemcpy(p->d_gen, blk.data(), blk.size() * 4, hipMemcpyHostToDevice) ==
+                     hipSuccess;
+        }
     }
-    ok = ok && hipMalloc(&p->d_err, 4) == hipSuccess &&
-         hipMemset(p->d_err, 0, 4) == hipSuccess;
     if (!ok) {
         qi_plan_destroy(p);
         return nullptr;
@@ -177,6 +179,7 @@ void qi_plan_destroy(qi_plan* p)
         (void)hipFree(p->d_gen);
     if (p->d_err)
         (void)hipFree(p->d_err);
+    ntt_plan_free(p);
     p->host.release();
     delete p;
 }

@@ -30,6 +30,8 @@ namespace qi {
 
 long long ctx_stride(const qi_plan* p, long long words)
 {
+    if (p->ntt)
+        return ntt_ctx_words(p);
     const MatLayout L = ctx_layout(p);
     return static_cast<long long>(L.words()) + 2 * L.KP +
            route_tiles(words) * kRouteStride + slow_words(words);
@@ -44,47 +46,24 @@ SlowList ctx_slow(const qi_plan* p, const void* d_ctx, long long words)
                     ctx_stride(p, words)};
 }
 
-// Decode contexts for n_stripes stripes: interpolation matrices + OOR route
-// tables.  k <= 64 on the device; otherwise the matrices are built on the
-// host from h_ids and the route tables are marked "scan the buckets".
-int build_ctx(qi_plan* p, const uint16_t* d_ids, const uint16_t* h_ids,
-              int n_stripes, const Oor* in, int slot_base, int by_pos,
-              long long words, void* d_ctx, hipStream_t s)
+// Decode contexts for n_stripes stripes, built on the device inside the
+// caller's stream: k <= 64, interpolation matrices + OOR route tables
+// (decode_ctx_kernel); k > 64, the NTT decode's per-pattern constants
+// (ntt_ctx_kernel; its decode reads the OOR buckets directly).
+int build_ctx(qi_plan* p, const uint16_t* d_ids, int n_stripes, const Oor* in,
+              int slot_base, int by_pos, long long words, void* d_ctx, hipStream_t s)
 {
     if (n_stripes == 0)
         return 0;
-    const MatLayout L = ctx_layout(p);
-    if (L.KP < 0)
-        return -3;
-    const int mode = p->sys ? 1 : 0;
-    const long long cs = ctx_stride(p, words);
-    if (p->k <= 64 && d_ids)
-        return launch_decode_ctx(p->k, p->r, mode, L, d_ids, n_stripes,
-                                 static_cast<int32_t*>(d_ctx), cs, in, slot_base,
-                                 by_pos, words, p->d_err, s);
-    if (!h_ids)
+    if (!d_ids)
         return -1;
-    std::vector<int32_t> blk(static_cast<size_t>(cs) * n_stripes, 0);
-    std::vector<uint32_t> ids(p->k), ev(p->k);
-    for (int t = 0; t < p->k; t++)
-        ev[t] = powmod_c(p->r, static_cast<uint32_t>(t));
-    const long long nt = route_tiles(words);
-    for (int s_ = 0; s_ < n_stripes; s_++) {
-        for (int i = 0; i < p->k; i++)
-            ids[i] = h_ids[static_cast<size_t>(s_) * p->k + i];
-        std::vector<uint32_t> M =
-            lagrange_matrix(p->k, p->r, ids.data(), mode, ev.data(), p->k);
-        int32_t* b = blk.data() + cs * s_;
-        pack_matrix(L, M.data(), b);
-        for (int i = 0; i < p->k; i++)
-            b[L.words() + i] = static_cast<int32_t>(ids[i]);
-        for (long long t = 0; t < nt; t++)
-            b[L.words() + 2 * L.KP + t * kRouteStride] = kRouteCap + 1;  // scan
-    }
-    if (hipMemcpyAsync(d_ctx, blk.data(), blk.size() * 4, hipMemcpyHostToDevice,
-                       s) != hipSuccess)
-        return -2;
-    return hipStreamSynchronize(s) == hipSuccess ? 0 : -2;
+    const long long cs = ctx_stride(p, words);
+    if (p->ntt)
+        return ntt_build_ctx(p, d_ids, n_stripes, static_cast<int32_t*>(d_ctx), cs, s);
+    const MatLayout L = ctx_layout(p);
+    return launch_decode_ctx(p->k, p->r, p->sys ? 1 : 0, L, d_ids, n_stripes,
+                             static_cast<int32_t*>(d_ctx), cs, in, slot_base, by_pos,
+                             words, p->d_err, s);
 }
 
 }  // namespace qi
@@ -112,6 +91,9 @@ int qi_gpu_encode(qi_plan* p, const uint16_t* d_data, long long dss,
         return 0;
     Oor oor{d_counts, d_entries, p->n_outputs, cap};
     RowDst out{d_out, oss, ors};
+    if (p->ntt)
+        return ntt_encode(p, d_data, dss, drs, out, words, n_stripes,
+                          d_counts ? &oor : nullptr, st(stream));
     if (!p->d_gen)
         return launch_encode_fnt(p->k, p->n, p->n_outputs, p->d_twist, d_data,
                                  dss, drs, out, words, n_stripes, oor,
@@ -140,7 +122,8 @@ int qi_gpu_decode_ctx(qi_plan* p, const uint16_t* d_ids, const uint16_t* h_ids,
         return -1;
     Oor in{const_cast<uint32_t*>(d_counts), const_cast<uint32_t*>(d_entries),
            p->n_outputs, cap};
-    return qi::build_ctx(p, d_ids, h_ids, n_stripes, d_counts ? &in : nullptr,
+    (void)h_ids;  // contexts are built on the device for every k
+    return qi::build_ctx(p, d_ids, n_stripes, d_counts ? &in : nullptr,
                          p->sys ? p->k : 0, 0, words, d_ctx, st(stream));
 }
 
@@ -168,6 +151,9 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
     const long long cs = ctx_stride(p, words);
     const int32_t* ctx = static_cast<const int32_t*>(d_ctx);
     (void)d_ids;  // the context carries the ids (as dwords)
+    if (p->ntt)
+        return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, p->sys ? p->k : 0, out,
+                          words, n_stripes, st(stream));
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, p->sys ? p->k : 0,
                          nullptr,
@@ -184,8 +170,9 @@ int qi_gpu_decode_ctx_packed(qi_plan* p, const uint16_t* d_ids,
         return -1;
     Oor in{const_cast<uint32_t*>(d_counts), const_cast<uint32_t*>(d_entries),
            p->k, cap};
-    return qi::build_ctx(p, d_ids, h_ids, n_stripes, d_counts ? &in : nullptr, 0,
-                         1, words, d_ctx, st(stream));
+    (void)h_ids;
+    return qi::build_ctx(p, d_ids, n_stripes, d_counts ? &in : nullptr, 0, 1, words,
+                         d_ctx, st(stream));
 }
 
 int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
@@ -205,6 +192,9 @@ int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
     RowDst out{d_out, oss, ors};
     const long long cs = ctx_stride(p, words);
     const int32_t* ctx = static_cast<const int32_t*>(d_ctx);
+    if (p->ntt)
+        return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, 0, out, words,
+                          n_stripes, st(stream));
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, 0, nullptr,
                          reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),

@@ -63,9 +63,8 @@ namespace qi {
 // per-stripe decode context stride (int32 words) and builder (qi_gpu.cpp)
 long long ctx_stride(const qi_plan* p, long long words);
 SlowList ctx_slow(const qi_plan* p, const void* d_ctx, long long words);
-int build_ctx(qi_plan* p, const uint16_t* d_ids, const uint16_t* h_ids,
-              int n_stripes, const Oor* in, int slot_base, int by_pos,
-              long long words, void* d_ctx, hipStream_t s);
+int build_ctx(qi_plan* p, const uint16_t* d_ids, int n_stripes, const Oor* in,
+              int slot_base, int by_pos, long long words, void* d_ctx, hipStream_t s);
 }  // namespace qi
 
 struct qi_plan {
@@ -75,6 +74,26 @@ struct qi_plan {
     int32_t* d_twist = nullptr;  // encode twist factors (non-systematic)
     int32_t* d_gen = nullptr;    // generator matrix block (matrix encode)
     qi::MatLayout gen{0, 0, 0};
+    // general-k path (k > 64, ntt.hip): transforms of length <= nmax =
+    // max(n, len_2k), balanced twiddle tables w^e / w^-e, and the systematic
+    // encode's constant decode context
+    int ntt = 0, len2k = 0, nmax = 0;
+    int32_t* d_tw[2] = {nullptr, nullptr};
+    int32_t* d_sysctx = nullptr;
     uint32_t* d_err = nullptr;
     qi::HostState host;
 };
+
+namespace qi {
+// ---- general-k path (ntt.hip) ----
+int ntt_plan_init(qi_plan* p);
+void ntt_plan_free(qi_plan* p);
+long long ntt_ctx_words(const qi_plan* p);
+int ntt_build_ctx(const qi_plan* p, const uint16_t* d_ids, int n_stripes, int32_t* d_ctx,
+                  long long ctx_stride, hipStream_t s);
+int ntt_encode(const qi_plan* p, const uint16_t* data, long long dss, long long drs,
+               RowDst out, long long words, int n_stripes, const Oor* oor, hipStream_t s);
+int ntt_decode(const qi_plan* p, const int32_t* ctx, long long ctx_stride, RowSrc src,
+               const Oor* in_oor, int slot_base, RowDst out, long long words,
+               int n_stripes, hipStream_t s);
+}  // namespace qi

@@ -55,7 +55,7 @@ def craft_oor(ora, codec, data, rng, n_cols):
     cw = (C.c_uint32 * codec.n)()
     din = (C.c_uint32 * k)()
     ids = (C.c_uint32 * k)(*range(k))
-    ctx = C.create_string_buffer(8 * 1024 * 4 + 64)
+    ctx = C.create_string_buffer(4 + 16 * 4096 + 64)
     if codec.sys:
         ora.qo_ctx_init(C.byref(codec), ctx, ids)
 
@@ -87,7 +87,7 @@ def craft_oor(ora, codec, data, rng, n_cols):
         done += 1
 
 
-def gen_blocks(ref, ora, name, k, m, sys_, pkt, block_bytes, seed,
+def _gen_blocks(ref, ora, name, k, m, sys_, pkt, block_bytes, seed,
                n_patterns, n_craft, out_dir):
     rng = np.random.default_rng(seed)
     codec = Codec()
@@ -131,7 +131,7 @@ def gen_blocks(ref, ora, name, k, m, sys_, pkt, block_bytes, seed,
           f"oor={int(cnt.sum())}")
 
 
-def gen_cabi(ref, ora, name, k, m, sys_, block_bytes, seed, n_patterns,
+def _gen_cabi(ref, ora, name, k, m, sys_, block_bytes, seed, n_patterns,
              n_craft, out_dir):
     """C-ABI fixtures: full fragment buffers (FNT1 header + payload)."""
     rng = np.random.default_rng(seed)
@@ -190,6 +190,16 @@ def main():
     ora = C.CDLL(ORA)
     ora.qo_nth_root.restype = C.c_uint32
     out = HERE
+    # `python gen_golden.py name ...` regenerates only the named fixtures
+    only = set(sys.argv[1:])
+
+    def gen_blocks(*a):
+        if not only or a[2] in only:
+            _gen_blocks(*a)
+
+    def gen_cabi(*a):
+        if not only or a[2] in only:
+            _gen_cabi(*a)
     # block-level (vertical) fixtures; pkt sizes differ on purpose (outputs
     # are pkt-size invariant)
     gen_blocks(ref, ora, "blk_k4_m4", 4, 4, 0, 512, 4096 + 6, 11, 6, 8, out)
@@ -208,6 +218,15 @@ def main():
     gen_cabi(ref, ora, "cabi_k4_m4_big", 4, 4, 0, 2 * 65536 + 10, 25, 2, 12,
              out)
     gen_cabi(ref, ora, "cabi_k8_m4_sys", 8, 4, 1, 3 * 4096 + 2, 24, 6, 8, out)
+    # k > 64: the NTT-structured general path (round 2)
+    gen_blocks(ref, ora, "blk_k200_m56", 200, 56, 0, 1024, 1500 + 2, 31, 3, 12,
+               out)
+    gen_blocks(ref, ora, "blk_k200_m56_sys", 200, 56, 1, 512, 1500, 32, 3, 12,
+               out)
+    gen_blocks(ref, ora, "blk_k256_m768", 256, 768, 0, 256, 800, 33, 2, 12, out)
+    gen_blocks(ref, ora, "blk_k100_m28", 100, 28, 0, 64, 1200 + 6, 34, 3, 8, out)
+    gen_cabi(ref, ora, "cabi_k200_m56", 200, 56, 0, 1500 + 2, 35, 2, 8, out)
+    gen_cabi(ref, ora, "cabi_k130_m30_sys", 130, 30, 1, 2000, 36, 2, 8, out)
 
 
 if __name__ == "__main__":

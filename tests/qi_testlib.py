@@ -137,7 +137,7 @@ def craft_oor_columns(k, m, sys_, data_rows, rng, n_cols, rows=None, col_range=N
     first = k if sys_ else 0
     cw = (C.c_uint32 * c.n)()
     din = (C.c_uint32 * k)()
-    ctx = C.create_string_buffer(40000)
+    ctx = C.create_string_buffer(4 + 16 * 4096 + 64)
     if sys_:
         o.qo_ctx_init(C.byref(c), ctx, (C.c_uint32 * k)(*range(k)))
 

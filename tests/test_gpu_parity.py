@@ -219,11 +219,79 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
     (32, 32, 0, 2, 1024),
     (33, 31, 0, 2, 513),      # K = 64 codelet, k not a power of two
     (64, 960, 0, 2, 2048),    # cfg3 shape
-    (100, 28, 0, 1, 256),     # K = 128: matrix encode path, host ctx
+    # k > 64: the NTT-structured general path (ntt.hip)
+    (65, 63, 0, 2, 300),      # smallest general-path code
+    (100, 28, 0, 2, 1000),
+    (100, 50, 1, 2, 999),     # systematic: interpolation + NTT_n encode
+    (200, 56, 0, 3, 1000),    # quadiron_fnt32_new(2, 200, 56, ...)
+    (200, 56, 1, 2, 513),
+    (256, 768, 0, 2, 700),    # n = 1024, len_2k = 512
+    (130, 900, 1, 1, 300),    # systematic, n = 2048 > len_2k
+    (1000, 24, 0, 1, 260),    # len_2k = 2048 > n = 1024
 ])
 def test_batch_vs_oracle(k, m, sys_, S, P):
-    _batch_roundtrip(k, m, sys_, S, P, seed=k * 1000 + m + P,
-                     n_craft=16 if k <= 64 else 0)
+    _batch_roundtrip(k, m, sys_, S, P, seed=k * 1000 + m + P, n_craft=16)
+
+
+def _eval_rows(data, rows, n, sys_):
+    """Reference values of non-systematic output rows by direct evaluation
+    of the data polynomial at r^i (numpy, int64): (len(rows), P)."""
+    assert not sys_
+    k, P = data.shape
+    r = pow(3, 65536 // n, Q)
+    out = np.zeros((len(rows), P), np.int64)
+    for a, i in enumerate(rows):
+        x = pow(r, int(i), Q)
+        acc = np.zeros(P, np.int64)
+        for t in range(k - 1, -1, -1):
+            acc = (acc * x + data[t].astype(np.int64)) % Q
+        out[a] = acc
+    return out
+
+
+@pytest.mark.parametrize("k,m,sys_,S,P", [
+    (130, 16000, 0, 1, 4500),   # n = 16384: the columns run in 2 slices
+    (200, 56, 0, 600, 256),     # 600 stripes: 2 stripe groups per launch
+    (100, 16000, 1, 1, 4200),   # systematic, sliced
+])
+def test_general_path_slicing(k, m, sys_, S, P):
+    """The general path cuts a batch into column slices and stripe groups
+    (HBM scratch budget): OOR marks keep absolute columns, every stripe
+    round-trips, and sampled output rows match direct evaluation."""
+    torch = _torch()
+    import quadiron_amd as qa
+    rng = np.random.default_rng(k + m + S)
+    plan = qa.Plan(k, m, sys_)
+    no, n = plan.n_outputs, plan.n
+    data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
+    dd = torch.from_numpy(data.view(np.int16)).cuda()
+    out = torch.zeros((S, no, P), dtype=torch.int16, device="cuda")
+    cap = 64 + P // 64
+    counts = torch.zeros(S * no, dtype=torch.int32, device="cuda")
+    entries = torch.zeros(S * no * cap, dtype=torch.int32, device="cuda")
+    plan.encode(dd, out, counts, entries, cap)
+    torch.cuda.synchronize()
+    cnt_h = counts.cpu().numpy().view(np.uint32).reshape(S, no)
+    ent_h = entries.cpu().numpy().view(np.uint32).reshape(S, no, cap)
+    assert (cnt_h <= cap).all()
+    if not sys_:
+        rows = sorted({0, 1, no // 2, no - 1, *rng.integers(0, no, 4).tolist()})
+        o = out[0].cpu().numpy().view(np.uint16)
+        ref = _eval_rows(data[0], rows, n, sys_)
+        for a, i in enumerate(rows):
+            assert (o[i] == (ref[a] & 0xFFFF)).all(), i
+            marks = np.nonzero(ref[a] == 65536)[0]
+            assert (np.sort(ent_h[0, i, :cnt_h[0, i]]) == marks).all(), i
+    ids = np.zeros((S, k), np.uint16)
+    for s in range(S):
+        ids[s] = np.sort(rng.choice(k + m, k, replace=False))
+    di = torch.from_numpy(ids.view(np.int16)).cuda()
+    ctx = torch.zeros(plan.ctx_bytes(S, P), dtype=torch.uint8, device="cuda")
+    plan.decode_ctx(di, ctx, P, counts, entries, cap)
+    dec = torch.zeros((S, k, P), dtype=torch.int16, device="cuda")
+    assert plan.decode(ctx, di, out, dec, data=dd, counts=counts,
+                       entries=entries, cap=cap) == 0
+    assert torch.equal(dec, dd)
 
 
 @pytest.mark.parametrize("k,m,S,P", [

@@ -9,7 +9,7 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RES = os.path.join(ROOT, "build", "obj", "kernels.res")
+RES = [os.path.join(ROOT, "build", "obj", f) for f in ("kernels.res", "ntt.res")]
 
 # kernels allowed to use scratch: the adversarial-OOR recompute and the
 # K = 64 encode codelet (256 VGPRs at 2 waves/SIMD, 3-4 spilled registers;
@@ -18,10 +18,10 @@ ALLOWED = ("matrix_redo_kernel", "encode_fnt_kernelILi64E")
 
 
 def kernels():
-    if not os.path.exists(RES):
+    if not all(os.path.exists(r) for r in RES):
         pytest.skip("kernel resource report not built (make -C quadiron_amd/csrc)")
     out, cur = {}, None
-    for line in open(RES):
+    for line in (ln for r in RES for ln in open(r)):
         m = re.search(r"remark: Function Name: (\S+)", line)
         if m:
             cur = m.group(1)
@@ -36,7 +36,8 @@ def kernels():
 def test_report_lists_the_hot_kernels():
     ks = kernels()
     for name in ("encode_fnt_kernel", "matrix_mfma_kernel", "matrix_kernel",
-                 "decode_ctx_kernel", "matrix_redo_kernel"):
+                 "decode_ctx_kernel", "matrix_redo_kernel", "ntt_pass_kernel",
+                 "ntt_ctx_kernel", "ntt_expand_kernel", "ntt_fix_kernel"):
         assert any(name in k for k in ks), name
 
 
