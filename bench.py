@@ -45,6 +45,9 @@ CONFIGS = {
     "cfg2": (16, 48, 65536, 4096),
     "cfg3": (64, 960, 4096, 1024),   # high fragmentation, n = 1024
     "cfg1": (4, 4, 1024, 100),       # the reference's CPU plumbing case
+    # general path (k > 64, NTT passes): not BASELINE configs, extra lines
+    "k200": (200, 56, 65536, 64),    # n = 256, len_2k = 512
+    "k256": (256, 768, 4096, 256),   # n = 1024, len_2k = 512
 }
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 
@@ -390,9 +393,11 @@ def main(argv=None):
     metric = ("device-resident encode+decode GB/s per GPU, RS-FNT k=16 n=64 "
               "pkt=64KiB" if headline else
               f"device-resident encode+decode GB/s per GPU, {name}")
-    mat_kernel = "matrix_mfma_kernel<*>" if k <= 64 else "matrix_kernel<*>"
-    enc_kernel = (f"encode_fnt_kernel<{K},*>" if not sys_ and K <= 64
-                  else mat_kernel)
+    if k > 64:
+        enc_kernel = "ntt_pass_kernel<*> (whole encode call)"
+    else:
+        enc_kernel = (f"encode_fnt_kernel<{K},*>" if not sys_
+                      else "matrix_mfma_kernel<*>")
     out = {
         "metric": metric,
         "value": value,

@@ -128,13 +128,19 @@ QI_HD int32_t sext24(int32_t c)
 // compiler cannot strength-reduce a power-of-two twiddle into shift/and/ashr
 // sequences, which would also defeat the single SDWA v_sub of the following
 // fold (4 VALU instead of 2).  The s_mov is CSE'd/hoisted (SALU, no VALU).
+//
+// The multiply itself is also written out: the callers' interval plans
+// guarantee |x| < 2^23, but the compiler's own range analysis cannot follow
+// lazily reduced sums and fell back to the quarter-rate v_mul_lo_u32 for
+// ~20 of the ~150 twiddle multiplies of a 64-point pass.
 template <int32_t CB>
 QI_HD int32_t mul_const(int32_t x)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-    int32_t c;
+    int32_t c, r;
     asm("s_mov_b32 %0, %1" : "=s"(c) : "i"(CB));
-    return x * sext24(c);
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "s"(c), "v"(x));
+    return r;
 #else
     return x * CB;
 #endif

@@ -357,6 +357,282 @@ __global__ __launch_bounds__(kNttBlock) void ntt_fix_kernel(NttFixArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-resident engine (max(n, len_2k) <= kLdsMaxN): one workgroup runs every
+// transform of a tile of T columns of one stripe in LDS, so HBM sees only the
+// algorithmic bytes (the k input rows and the output rows).  The tile is an
+// nmax x T int32 image (element (position, column) at buf[pos T + col]);
+// radix <= 32 passes, with every lane on one column of one butterfly group:
+//   forward transforms: decimation in frequency (natural order in, output
+//     X[j] at position pos(j) -- a mixed-radix digit reversal);
+//   inverse transforms: decimation in time, the transposed passes in reverse
+//     order (input x[t] at pos(t), natural order out).
+// So INTT_n can take the received rows scattered to pos(id), NTT_2k's output
+// is directly INTT_2k's input (C[j] applied at pos(j)), and no reordering
+// pass is needed (src/fec_base.h:1418-1448 in this order).
+// ---------------------------------------------------------------------------
+constexpr int kLdsThreads = 512;
+constexpr int kLdsMaxN = 2048;
+constexpr int kLdsMaxPasses = 6;
+
+struct XfPlan {
+    int N, np;
+    int lgr[kLdsMaxPasses];  // log2 radix of pass q
+    int sh[kLdsMaxPasses];   // log2 s_q = log2(N / (R_0 ... R_q))
+};
+
+// x[t] of a transform lives at pos(t) (DIF output / DIT input order)
+__device__ __forceinline__ int xf_pos(const XfPlan& P, int t)
+{
+    int p = 0;
+    for (int q = 0; q < P.np; q++) {
+        p += (t & ((1 << P.lgr[q]) - 1)) << P.sh[q];
+        t >>= P.lgr[q];
+    }
+    return p;
+}
+__device__ __forceinline__ int xf_index(const XfPlan& P, int p)
+{
+    int t = 0, b = 0;
+    for (int q = 0; q < P.np; q++) {
+        t += ((p >> P.sh[q]) & ((1 << P.lgr[q]) - 1)) << b;
+        b += P.lgr[q];
+    }
+    return t;
+}
+
+enum : int { kLdsEnc = 0, kLdsSysEnc = 1, kLdsDec = 2, kLdsSysDec = 3 };
+
+struct NttLdsArgs {
+    int mode;
+    int k, n, len2k, nmax;
+    int lgT, tiles;
+    long long words;
+    XfPlan pn, p2k;
+    const int32_t* tw;  // nmax forward entries, then nmax inverse ones
+    RowSrc src;         // enc: data rows by position; dec: received rows
+    const int32_t* ctx; // decode context (sys encode: the plan's, cs = 0)
+    long long cs;
+    int ids_off, c_off, pos_off;
+    Oor in_oor;
+    int slot_base;
+    uint16_t* out;      // output row r of stripe s at out + s*oss + r*ors
+    long long oss, ors;
+    int out_first, out_rows;  // sequence index of output row 0, row count
+    Oor out_oor;
+    uint32_t* err;
+};
+
+// One pass over the image: tasks (group start b, offset j < s) of the R
+// positions b + j + q s, lane = column.  DIF: codelet, then output u times
+// w_L^{j u}; DIT: input q times w_L^{+-j q}, then codelet.
+template <int R, bool DIF, bool INV>
+__device__ __forceinline__ void lds_pass(int32_t* buf, const int32_t* tw, int N, int lgs,
+                                         int lgL, int lgnmax, int lgT, int col, int g,
+                                         int G)
+{
+    const int s = 1 << lgs, tasks = N / R;
+    for (int tt = g; tt < tasks; tt += G) {
+        const int j = tt & (s - 1);
+        const int b = (tt >> lgs) << lgL;
+        int32_t v[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            int32_t x = buf[((b + j + q * s) << lgT) + col];
+            if (!DIF && q > 0 && j > 0)
+                x = mul_rt(x, tw[(j * q) << (lgnmax - lgL)]);
+            v[q] = x;
+        }
+        dft<R, kInLo, kInHi>(v);
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            int32_t y = v[INV ? (R - u) % R : u];
+            if (DIF && u > 0 && j > 0)
+                y = mul_rt(y, tw[(j * u) << (lgnmax - lgL)]);
+            buf[((b + j + u * s) << lgT) + col] = y;
+        }
+    }
+}
+
+template <bool DIF, bool INV>
+__device__ void lds_transform(int32_t* buf, const int32_t* tw, const XfPlan& P, int lgnmax,
+                              int lgT, int col, int g, int G)
+{
+    int lgN = 0;
+    while ((1 << lgN) < P.N)
+        lgN++;
+    for (int i = 0; i < P.np; i++) {
+        const int q = DIF ? i : P.np - 1 - i;  // DIT: the passes in reverse
+        const int lgs = P.sh[q], lgL = lgs + P.lgr[q];
+        switch (P.lgr[q]) {
+        case 1:
+            lds_pass<2, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            break;
+        case 2:
+            lds_pass<4, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            break;
+        case 3:
+            lds_pass<8, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            break;
+        case 4:
+            lds_pass<16, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            break;
+        default:
+            lds_pass<32, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            break;
+        }
+        __syncthreads();
+    }
+}
+
+// LDS side arrays behind the nmax x T image (int32 words)
+__host__ __device__ inline int lds_side_words(int nmax, int k, int len2k)
+{
+    return 2 * nmax + 2 * k + len2k;
+}
+
+constexpr int kLdsBatch = 8;  // row loads in flight per thread
+
+__global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
+{
+    extern __shared__ int32_t qi_ntt_lds[];
+    const int nmax = a.nmax, lgT = a.lgT, T = 1 << lgT, k = a.k;
+    int32_t* buf = qi_ntt_lds;
+    int32_t* tw = qi_ntt_lds + (nmax << lgT);  // forward, then inverse
+    int32_t* s_inv = tw + 2 * nmax;            // inv_A_i (balanced)
+    int32_t* s_id = s_inv + k;                 // received ids z_i
+    int32_t* s_c = s_id + k;                   // C[j] (balanced), natural order
+    const int s = blockIdx.x / a.tiles;
+    const long long c0 = static_cast<long long>(blockIdx.x - s * a.tiles) << lgT;
+    const int tid = threadIdx.x, col = tid & (T - 1), g = tid >> lgT, G = kLdsThreads >> lgT;
+    const long long cg = c0 + col;
+    const bool valid = cg < a.words;
+    int lgnmax = 0;
+    while ((1 << lgnmax) < nmax)
+        lgnmax++;
+    const bool dec = a.mode != kLdsEnc;
+    // every per-stripe constant into LDS first (one round of independent
+    // loads), so the hot loops below wait on nothing but their row loads
+    const int32_t* ctx = a.ctx + s * a.cs;
+    for (int e = tid; e < 2 * nmax; e += kLdsThreads)
+        tw[e] = a.tw[e];
+    if (dec) {
+        for (int i = tid; i < k; i += kLdsThreads) {
+            s_inv[i] = balanced(static_cast<uint32_t>(ctx[i]));
+            s_id[i] = ctx[a.ids_off + i];
+        }
+        for (int j = tid; j < a.len2k; j += kLdsThreads)
+            s_c[j] = balanced(static_cast<uint32_t>(ctx[a.c_off + j]));
+    }
+    const RowSrc& src = a.src;
+    auto row_ptr = [&](int id) {
+        return id < src.split ? src.base0 + s * src.ss0 + id * src.rs0
+                              : src.base1 + s * src.ss1 + (id - src.split) * src.rs1;
+    };
+    if (!dec) {
+        // data rows t < k at natural positions, zero above (DIF input);
+        // kLdsBatch row loads in flight per thread
+        for (int p0 = g; p0 < a.n; p0 += G * kLdsBatch) {
+            int32_t x[kLdsBatch];
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) {
+                const int p = p0 + u * G;
+                x[u] = (p < k && valid) ? row_ptr(p)[cg] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) {
+                const int p = p0 + u * G;
+                if (p < a.n)
+                    buf[(p << lgT) + col] = x[u];
+            }
+        }
+        __syncthreads();
+        lds_transform<true, false>(buf, tw, a.pn, lgnmax, lgT, col, g, G);
+    } else {
+        // INTT_n input (DIT order): zero, then y_i = v_i inv_A_i at pos_n(z_i)
+        for (int p = g; p < a.n; p += G)
+            buf[(p << lgT) + col] = 0;
+        __syncthreads();
+        for (int i0 = g; i0 < k; i0 += G * kLdsBatch) {
+            int32_t x[kLdsBatch];
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) {
+                const int i = i0 + u * G;
+                x[u] = 0;
+                if (i < k && valid)
+                    x[u] = row_ptr(src.by_pos ? i : s_id[i])[cg];
+            }
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) {
+                const int i = i0 + u * G;
+                if (i < k)
+                    buf[(xf_pos(a.pn, s_id[i]) << lgT) + col] = mul_rt(x[u], s_inv[i]);
+            }
+        }
+        __syncthreads();
+        if (a.in_oor.counts) {
+            // decode_prepare (src/fec_base.h:1361-1404): a marked symbol is
+            // 65536 = -1, so y = -inv_A_i at the marks inside this tile
+            for (int i = tid; i < k; i += kLdsThreads) {
+                const int id = s_id[i];  // sequence index z_i
+                const int slot = src.by_pos ? i : id - a.slot_base;
+                if (slot < 0)
+                    continue;  // systematic data row: no marks
+                const long long bk = static_cast<long long>(s) * a.in_oor.slots + slot;
+                uint32_t cnt = a.in_oor.counts[bk];
+                if (cnt > static_cast<uint32_t>(a.in_oor.cap)) {
+                    atomicOr(a.err, kErrOorTruncated);
+                    cnt = static_cast<uint32_t>(a.in_oor.cap);
+                }
+                const int p = xf_pos(a.pn, id);
+                const int32_t y = -s_inv[i];  // -inv_A_i, balanced
+                for (uint32_t e = 0; e < cnt; e++) {
+                    const long long c = static_cast<long long>(
+                                            a.in_oor.entries[bk * a.in_oor.cap + e]) - c0;
+                    if (c >= 0 && c < T)
+                        buf[(p << lgT) + static_cast<int>(c)] = y;
+                }
+            }
+            __syncthreads();
+        }
+        lds_transform<false, true>(buf, tw + nmax, a.pn, lgnmax, lgT, col, g, G);
+        // first k outputs, zero-extended to len_2k; NTT_2k (DIF)
+        for (int p = k + g; p < a.len2k; p += G)
+            buf[(p << lgT) + col] = 0;
+        __syncthreads();
+        lds_transform<true, false>(buf, tw, a.p2k, lgnmax, lgT, col, g, G);
+        // x C[j] (X[j] sits at pos_2k(j))
+        for (int p = g; p < a.len2k; p += G)
+            buf[(p << lgT) + col] = mul_rt(buf[(p << lgT) + col], s_c[xf_index(a.p2k, p)]);
+        __syncthreads();
+        lds_transform<false, true>(buf, tw + nmax, a.p2k, lgnmax, lgT, col, g, G);
+        if (a.mode != kLdsDec) {
+            // systematic: evaluate the coefficients at r^t (NTT_n, DIF)
+            for (int p = k + g; p < a.n; p += G)
+                buf[(p << lgT) + col] = 0;
+            __syncthreads();
+            lds_transform<true, false>(buf, tw, a.pn, lgnmax, lgT, col, g, G);
+        }
+    }
+    // output rows: sequence index t = out_first + r, at position t (DIT
+    // output: natural order) or pos_n(t) (DIF output)
+    if (!valid)
+        return;
+    const bool natural = a.mode == kLdsDec;
+    for (int r = g; r < a.out_rows; r += G) {
+        const int t = a.out_first + r;
+        const int p = natural ? t : xf_pos(a.pn, t);
+        const uint32_t cv = canon_vr(buf[(p << lgT) + col]);
+        a.out[s * a.oss + r * a.ors + cg] = static_cast<uint16_t>(cv);
+        if (cv == 65536u && a.out_oor.counts) {
+            const long long bk = static_cast<long long>(s) * a.out_oor.slots + r;
+            const uint32_t e = atomicAdd(&a.out_oor.counts[bk], 1u);
+            if (e < static_cast<uint32_t>(a.out_oor.cap))
+                a.out_oor.entries[bk * a.out_oor.cap + e] = static_cast<uint32_t>(cg);
+        }
+    }
+}
+
 namespace {
 
 int ilog2i(long long v)
@@ -462,6 +738,67 @@ struct Scratch {
 NttCtxLayout ctx_layout_of(const qi_plan* p)
 {
     return NttCtxLayout{p->k, p->n, p->len2k};
+}
+
+// radices <= 32 for the LDS passes, as even as possible (fewest twiddled
+// passes)
+XfPlan xf_plan(int N)
+{
+    XfPlan P{};
+    P.N = N;
+    const int bits = ilog2i(N);
+    P.np = std::max(1, (bits + 4) / 5);
+    int left = bits, sh = bits;
+    for (int q = 0; q < P.np; q++) {
+        const int b = (left + (P.np - q) - 1) / (P.np - q);
+        P.lgr[q] = b;
+        sh -= b;
+        P.sh[q] = sh;
+        left -= b;
+    }
+    return P;
+}
+
+bool lds_engine(const qi_plan* p)
+{
+    return p->nmax <= kLdsMaxN;
+}
+
+// columns per workgroup: a 64 KiB image (128 KiB at nmax = 2048)
+int lds_lgT(const qi_plan* p)
+{
+    const int lgn = ilog2i(p->nmax);
+    return std::min(6, std::max(4, 14 - lgn));
+}
+
+int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
+{
+    a.k = p->k;
+    a.n = p->n;
+    a.len2k = p->len2k;
+    a.nmax = p->nmax;
+    a.lgT = lds_lgT(p);
+    a.pn = xf_plan(p->n);
+    a.p2k = xf_plan(p->len2k);
+    a.tw = p->d_tw[0];
+    const NttCtxLayout L = ctx_layout_of(p);
+    a.ids_off = static_cast<int>(L.ids_off());
+    a.c_off = static_cast<int>(L.c_off());
+    a.pos_off = static_cast<int>(L.pos_off());
+    const long long tiles = (a.words + (1LL << a.lgT) - 1) >> a.lgT;
+    if (tiles * S > 0x7fffffffLL)
+        return -3;
+    a.tiles = static_cast<int>(tiles);
+    const size_t lds = ((static_cast<size_t>(p->nmax) << a.lgT) +
+                        lds_side_words(p->nmax, p->k, p->len2k)) * 4;
+    if (lds > 65536 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_lds_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(lds)) != hipSuccess)
+        return -2;
+    hipLaunchKernelGGL(ntt_lds_kernel, dim3(static_cast<unsigned>(tiles * S)),
+                       dim3(kLdsThreads), lds, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 RowSrc offset_src(RowSrc s, int sg0, long long c0)
@@ -606,6 +943,23 @@ int ntt_encode(const qi_plan* p, const uint16_t* data, long long dss, long long 
 {
     if (S <= 0 || words <= 0)
         return 0;
+    if (lds_engine(p)) {
+        NttLdsArgs a{};
+        a.mode = p->sys ? kLdsSysEnc : kLdsEnc;
+        a.words = words;
+        a.src = RowSrc{data, dss, drs, 1 << 30, nullptr, 0, 0, 1, p->k, 0};
+        a.ctx = p->sys ? p->d_sysctx : nullptr;
+        a.cs = 0;
+        a.out = out.base;
+        a.oss = out.ss;
+        a.ors = out.rs;
+        a.out_first = p->sys ? p->k : 0;
+        a.out_rows = p->n_outputs;
+        if (oor && oor->counts)
+            a.out_oor = *oor;
+        a.err = p->d_err;
+        return lds_launch(p, a, S, st);
+    }
     const Slicing sl = slicing(p, words, S);
     const long long sss = static_cast<long long>(p->nmax) * sl.W;
     Scratch sa, sb;
@@ -675,6 +1029,24 @@ int ntt_decode(const qi_plan* p, const int32_t* ctx, long long cs, RowSrc src,
 {
     if (S <= 0 || words <= 0)
         return 0;
+    if (lds_engine(p)) {
+        NttLdsArgs a{};
+        a.mode = p->sys ? kLdsSysDec : kLdsDec;
+        a.words = words;
+        a.src = src;
+        a.ctx = ctx;
+        a.cs = cs;
+        if (in_oor && in_oor->counts)
+            a.in_oor = *in_oor;
+        a.slot_base = slot_base;
+        a.out = out.base;
+        a.oss = out.ss;
+        a.ors = out.rs;
+        a.out_first = 0;
+        a.out_rows = p->k;
+        a.err = p->d_err;
+        return lds_launch(p, a, S, st);
+    }
     const Slicing sl = slicing(p, words, S);
     const long long sss = static_cast<long long>(p->nmax) * sl.W;
     Scratch sa, sb;

@@ -251,13 +251,15 @@ def _eval_rows(data, rows, n, sys_):
 
 @pytest.mark.parametrize("k,m,sys_,S,P", [
     (130, 16000, 0, 1, 4500),   # n = 16384: the columns run in 2 slices
-    (200, 56, 0, 600, 256),     # 600 stripes: 2 stripe groups per launch
+    (100, 3000, 0, 70, 256),    # n = 4096, 70 stripes: 2 stripe groups
+    (200, 56, 0, 600, 256),     # LDS engine over 600 stripes x 8 tiles
     (100, 16000, 1, 1, 4200),   # systematic, sliced
 ])
 def test_general_path_slicing(k, m, sys_, S, P):
-    """The general path cuts a batch into column slices and stripe groups
-    (HBM scratch budget): OOR marks keep absolute columns, every stripe
-    round-trips, and sampled output rows match direct evaluation."""
+    """The general path's multi-pass engine (max(n, len_2k) > 2048) cuts a
+    batch into column slices and stripe groups (HBM scratch budget): OOR
+    marks keep absolute columns, every stripe round-trips, and sampled output
+    rows match direct evaluation (the LDS engine below that size too)."""
     torch = _torch()
     import quadiron_amd as qa
     rng = np.random.default_rng(k + m + S)
