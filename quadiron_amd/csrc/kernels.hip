@@ -1375,8 +1375,11 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
     // limited the kernel to 4 workgroups per CU
     extern __shared__ uint32_t qi_ctx_lds[];
+    // rows at an odd pitch: the 4-lanes-per-row passes below read 16 rows
+    // per wave, which a pitch of k (a power of two) put in one LDS bank
+    const int kp = k | 1;
     uint32_t* Mt = qi_ctx_lds;
-    uint32_t* Qt = qi_ctx_lds + k * k;
+    uint32_t* Qt = qi_ctx_lds + k * kp;
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
     int32_t* mat = ctx + s * ctx_stride;
@@ -1446,10 +1449,10 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         uint32_t q = 1;  // A[k]
         uint32_t* dst = mode == 0 ? Mt : Qt;
         const uint32_t sc = mode == 0 ? inv : 1u;
-        dst[(k - 1) * k + tid] = sc;
+        dst[(k - 1) * kp + tid] = sc;
         for (int j = k - 1; j >= 1; j--) {
             q = addm(A[j], mulm(xi, q));
-            dst[(j - 1) * k + tid] = mulm(q, sc);
+            dst[(j - 1) * kp + tid] = mulm(q, sc);
         }
         if (mode != 0) {
             // M[t][i] = Q_i(r^t) / A'(x_i)
@@ -1457,8 +1460,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             for (int t = 0; t < k; t++) {
                 uint32_t acc = 0;
                 for (int j = k - 1; j >= 0; j--)
-                    acc = addm(mulm(acc, e), Qt[j * k + tid]);
-                Mt[t * k + tid] = mulm(acc, inv);
+                    acc = addm(mulm(acc, e), Qt[j * kp + tid]);
+                Mt[t * kp + tid] = mulm(acc, inv);
                 e = mulm(e, r);
             }
         }
@@ -1467,7 +1470,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // 4 lanes per row: pack_row's work split over the row's entries, its
     // reductions over the 4 lanes (k = 64: 92 -> 62 us per 1024 stripes)
     for (int t = tid / 4; t < L.R; t += NT / 4)
-        pack_row_g4(Mt + t * k, L, t, mat, tid & 3);
+        pack_row_g4(Mt + t * kp, L, t, mat, tid & 3);
     if (L.KS()) {
         // the matrix-core operand tiles, from the row-scaled entries in LDS
         __syncthreads();
@@ -1485,7 +1488,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                 for (int jb = 0; jb < 4; jb++) {
                     if (i0 + jb < k) {
                         int32_t a, b;
-                        split_i8(static_cast<uint32_t>(rows[t * k + i0 + jb]), a, b);
+                        split_i8(static_cast<uint32_t>(rows[t * kp + i0 + jb]), a, b);
                         aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
                         bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
                     }
@@ -1788,7 +1791,7 @@ int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
     if (k > 64 || S <= 0)
         return -3;
     Oor none{nullptr, nullptr, 0, 0};
-    const size_t lds = static_cast<size_t>(k) * k * 4 * (mode ? 2 : 1);
+    const size_t lds = static_cast<size_t>(k) * (k | 1) * 4 * (mode ? 2 : 1);
     if (k > 32)
         hipLaunchKernelGGL(decode_ctx_kernel<256>, dim3(S), dim3(256), lds, st, k, r,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,

@@ -64,9 +64,13 @@ constexpr int kMaxPasses = 16;
 // [-65536, 65535].
 __device__ __forceinline__ int32_t mul_rt(int32_t x, int32_t c)
 {
-    const long long p = static_cast<long long>(sext24(x)) * static_cast<long long>(sext24(c));
-    const uint32_t lo = static_cast<uint32_t>(p);
-    const int32_t hi = static_cast<int32_t>(p >> 32);
+    // the two halves written out: the operands are known to fit 24 bits,
+    // which the compiler cannot see through the lazily reduced values (it
+    // sign-extended both first)
+    uint32_t lo;
+    int32_t hi;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(lo) : "v"(x), "v"(c));
+    asm("v_mul_hi_i32_i24 %0, %1, %2" : "=v"(hi) : "v"(x), "v"(c));
     return static_cast<int32_t>(lo & 0xffffu) - static_cast<int32_t>(lo >> 16) + hi;
 }
 
@@ -379,6 +383,8 @@ struct XfPlan {
     int N, np;
     int lgr[kLdsMaxPasses];  // log2 radix of pass q
     int sh[kLdsMaxPasses];   // log2 s_q = log2(N / (R_0 ... R_q))
+    int tw[kLdsMaxPasses];   // pass q's twiddles in the LDS table: entry
+                             // j R_q + u = w_{L_q}^{+-j u}, j < s_q
 };
 
 // x[t] of a transform lives at pos(t) (DIF output / DIT input order)
@@ -408,8 +414,10 @@ struct NttLdsArgs {
     int k, n, len2k, nmax;
     int lgT, tiles;
     long long words;
-    XfPlan pn, p2k;
-    const int32_t* tw;  // nmax forward entries, then nmax inverse ones
+    // NTT_n / INTT_n / NTT_2k / INTT_2k: geometry + pass table offsets
+    XfPlan pnf, pni, p2f, p2i;
+    const int32_t* tw;  // the pass twiddle tables (qi_plan::d_ldstw)
+    int tw_words;
     RowSrc src;         // enc: data rows by position; dec: received rows
     const int32_t* ctx; // decode context (sys encode: the plan's, cs = 0)
     long long cs;
@@ -425,60 +433,63 @@ struct NttLdsArgs {
 
 // One pass over the image: tasks (group start b, offset j < s) of the R
 // positions b + j + q s, lane = column.  DIF: codelet, then output u times
-// w_L^{j u}; DIT: input q times w_L^{+-j q}, then codelet.
+// w_L^{j u}; DIT: input q times w_L^{+-j q}, then codelet.  A task's
+// twiddles are contiguous in the pass table (vector LDS reads) and its R
+// elements sit at one base plus loop-invariant strides.
 template <int R, bool DIF, bool INV>
-__device__ __forceinline__ void lds_pass(int32_t* buf, const int32_t* tw, int N, int lgs,
-                                         int lgL, int lgnmax, int lgT, int col, int g,
-                                         int G)
+__device__ __forceinline__ void lds_pass(int32_t* buf, const int32_t* twp, int N, int lgs,
+                                         int lgL, int lgT, int col, int g, int G)
 {
-    const int s = 1 << lgs, tasks = N / R;
+    const int tasks = N / R, sE = (1 << lgs) << lgT;
     for (int tt = g; tt < tasks; tt += G) {
-        const int j = tt & (s - 1);
-        const int b = (tt >> lgs) << lgL;
-        int32_t v[R];
+        const int j = tt & ((1 << lgs) - 1);
+        int32_t* e = buf + ((((tt >> lgs) << lgL) + j) << lgT) + col;
+        const int32_t* tj = twp + j * R;
+        int32_t v[R], w[R];
 #pragma unroll
         for (int q = 0; q < R; q++) {
-            int32_t x = buf[((b + j + q * s) << lgT) + col];
-            if (!DIF && q > 0 && j > 0)
-                x = mul_rt(x, tw[(j * q) << (lgnmax - lgL)]);
-            v[q] = x;
+            v[q] = e[q * sE];
+            w[q] = tj[q];
+        }
+        if (!DIF) {
+#pragma unroll
+            for (int q = 1; q < R; q++)
+                v[q] = mul_rt(v[q], w[q]);
         }
         dft<R, kInLo, kInHi>(v);
 #pragma unroll
         for (int u = 0; u < R; u++) {
             int32_t y = v[INV ? (R - u) % R : u];
-            if (DIF && u > 0 && j > 0)
-                y = mul_rt(y, tw[(j * u) << (lgnmax - lgL)]);
-            buf[((b + j + u * s) << lgT) + col] = y;
+            if (DIF && u > 0)
+                y = mul_rt(y, w[u]);
+            e[u * sE] = y;
         }
     }
 }
 
 template <bool DIF, bool INV>
-__device__ void lds_transform(int32_t* buf, const int32_t* tw, const XfPlan& P, int lgnmax,
-                              int lgT, int col, int g, int G)
+__device__ void lds_transform(int32_t* buf, const int32_t* tw, const XfPlan& P, int lgT,
+                              int col, int g, int G)
 {
-    int lgN = 0;
-    while ((1 << lgN) < P.N)
-        lgN++;
     for (int i = 0; i < P.np; i++) {
         const int q = DIF ? i : P.np - 1 - i;  // DIT: the passes in reverse
         const int lgs = P.sh[q], lgL = lgs + P.lgr[q];
+        const int32_t* twp = tw + P.tw[q];
         switch (P.lgr[q]) {
         case 1:
-            lds_pass<2, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            lds_pass<2, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
             break;
         case 2:
-            lds_pass<4, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            lds_pass<4, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
             break;
         case 3:
-            lds_pass<8, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            lds_pass<8, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
             break;
         case 4:
-            lds_pass<16, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            lds_pass<16, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
             break;
         default:
-            lds_pass<32, DIF, INV>(buf, tw, P.N, lgs, lgL, lgnmax, lgT, col, g, G);
+            lds_pass<32, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
             break;
         }
         __syncthreads();
@@ -486,9 +497,9 @@ __device__ void lds_transform(int32_t* buf, const int32_t* tw, const XfPlan& P, 
 }
 
 // LDS side arrays behind the nmax x T image (int32 words)
-__host__ __device__ inline int lds_side_words(int nmax, int k, int len2k)
+__host__ __device__ inline int lds_side_words(int tw_words, int k, int len2k)
 {
-    return 2 * nmax + 2 * k + len2k;
+    return tw_words + 2 * k + len2k;
 }
 
 constexpr int kLdsBatch = 8;  // row loads in flight per thread
@@ -498,8 +509,8 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     extern __shared__ int32_t qi_ntt_lds[];
     const int nmax = a.nmax, lgT = a.lgT, T = 1 << lgT, k = a.k;
     int32_t* buf = qi_ntt_lds;
-    int32_t* tw = qi_ntt_lds + (nmax << lgT);  // forward, then inverse
-    int32_t* s_inv = tw + 2 * nmax;            // inv_A_i (balanced)
+    int32_t* tw = qi_ntt_lds + (nmax << lgT);  // pass twiddle tables
+    int32_t* s_inv = tw + a.tw_words;          // inv_A_i (balanced)
     int32_t* s_id = s_inv + k;                 // received ids z_i
     int32_t* s_c = s_id + k;                   // C[j] (balanced), natural order
     const int s = blockIdx.x / a.tiles;
@@ -507,14 +518,11 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     const int tid = threadIdx.x, col = tid & (T - 1), g = tid >> lgT, G = kLdsThreads >> lgT;
     const long long cg = c0 + col;
     const bool valid = cg < a.words;
-    int lgnmax = 0;
-    while ((1 << lgnmax) < nmax)
-        lgnmax++;
     const bool dec = a.mode != kLdsEnc;
     // every per-stripe constant into LDS first (one round of independent
     // loads), so the hot loops below wait on nothing but their row loads
     const int32_t* ctx = a.ctx + s * a.cs;
-    for (int e = tid; e < 2 * nmax; e += kLdsThreads)
+    for (int e = tid; e < a.tw_words; e += kLdsThreads)
         tw[e] = a.tw[e];
     if (dec) {
         for (int i = tid; i < k; i += kLdsThreads) {
@@ -547,7 +555,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
             }
         }
         __syncthreads();
-        lds_transform<true, false>(buf, tw, a.pn, lgnmax, lgT, col, g, G);
+        lds_transform<true, false>(buf, tw, a.pnf, lgT, col, g, G);
     } else {
         // INTT_n input (DIT order): zero, then y_i = v_i inv_A_i at pos_n(z_i)
         for (int p = g; p < a.n; p += G)
@@ -566,7 +574,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
             for (int u = 0; u < kLdsBatch; u++) {
                 const int i = i0 + u * G;
                 if (i < k)
-                    buf[(xf_pos(a.pn, s_id[i]) << lgT) + col] = mul_rt(x[u], s_inv[i]);
+                    buf[(xf_pos(a.pnf, s_id[i]) << lgT) + col] = mul_rt(x[u], s_inv[i]);
             }
         }
         __syncthreads();
@@ -584,7 +592,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
                     atomicOr(a.err, kErrOorTruncated);
                     cnt = static_cast<uint32_t>(a.in_oor.cap);
                 }
-                const int p = xf_pos(a.pn, id);
+                const int p = xf_pos(a.pnf, id);
                 const int32_t y = -s_inv[i];  // -inv_A_i, balanced
                 for (uint32_t e = 0; e < cnt; e++) {
                     const long long c = static_cast<long long>(
@@ -595,23 +603,23 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
             }
             __syncthreads();
         }
-        lds_transform<false, true>(buf, tw + nmax, a.pn, lgnmax, lgT, col, g, G);
+        lds_transform<false, true>(buf, tw, a.pni, lgT, col, g, G);
         // first k outputs, zero-extended to len_2k; NTT_2k (DIF)
         for (int p = k + g; p < a.len2k; p += G)
             buf[(p << lgT) + col] = 0;
         __syncthreads();
-        lds_transform<true, false>(buf, tw, a.p2k, lgnmax, lgT, col, g, G);
+        lds_transform<true, false>(buf, tw, a.p2f, lgT, col, g, G);
         // x C[j] (X[j] sits at pos_2k(j))
         for (int p = g; p < a.len2k; p += G)
-            buf[(p << lgT) + col] = mul_rt(buf[(p << lgT) + col], s_c[xf_index(a.p2k, p)]);
+            buf[(p << lgT) + col] = mul_rt(buf[(p << lgT) + col], s_c[xf_index(a.p2f, p)]);
         __syncthreads();
-        lds_transform<false, true>(buf, tw + nmax, a.p2k, lgnmax, lgT, col, g, G);
+        lds_transform<false, true>(buf, tw, a.p2i, lgT, col, g, G);
         if (a.mode != kLdsDec) {
             // systematic: evaluate the coefficients at r^t (NTT_n, DIF)
             for (int p = k + g; p < a.n; p += G)
                 buf[(p << lgT) + col] = 0;
             __syncthreads();
-            lds_transform<true, false>(buf, tw, a.pn, lgnmax, lgT, col, g, G);
+            lds_transform<true, false>(buf, tw, a.pnf, lgT, col, g, G);
         }
     }
     // output rows: sequence index t = out_first + r, at position t (DIT
@@ -621,7 +629,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     const bool natural = a.mode == kLdsDec;
     for (int r = g; r < a.out_rows; r += G) {
         const int t = a.out_first + r;
-        const int p = natural ? t : xf_pos(a.pn, t);
+        const int p = natural ? t : xf_pos(a.pnf, t);
         const uint32_t cv = canon_vr(buf[(p << lgT) + col]);
         a.out[s * a.oss + r * a.ors + cg] = static_cast<uint16_t>(cv);
         if (cv == 65536u && a.out_oor.counts) {
@@ -759,16 +767,82 @@ XfPlan xf_plan(int N)
     return P;
 }
 
-bool lds_engine(const qi_plan* p)
+// The four transforms' pass twiddle tables, back to back (offsets kept 4-
+// aligned for the vector LDS reads): pass q of a length-N transform holds
+// w_{L_q}^{+-j u} at j R_q + u, with w_L = w_nmax^{nmax / L}.  Fills `tab`
+// when given; returns the total words.
+// Order INTT_n, NTT_2k, INTT_2k, NTT_n: a decode stages the first three, a
+// non-systematic encode the last one, systematic codes all four.
+enum : int { kTwPni = 0, kTwP2f = 1, kTwP2i = 2, kTwPnf = 3 };
+
+int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab)
 {
-    return p->nmax <= kLdsMaxN;
+    const uint32_t w = root_of_unity(static_cast<uint32_t>(p->nmax));
+    const int Ns[4] = {p->n, p->len2k, p->len2k, p->n};
+    const bool invs[4] = {true, false, true, false};
+    int off = 0;
+    for (int t = 0; t < 4; t++) {
+        pl[t] = xf_plan(Ns[t]);
+        const bool inv = invs[t];
+        for (int q = 0; q < pl[t].np; q++) {
+            const int R = 1 << pl[t].lgr[q], sq = 1 << pl[t].sh[q], L = R * sq;
+            pl[t].tw[q] = off;
+            if (tab) {
+                tab->resize(off + L);
+                const uint32_t wl = powmod_c(w, static_cast<uint32_t>(p->nmax / L));
+                const uint32_t wb = inv ? invmod_c(wl) : wl;
+                for (int j = 0; j < sq; j++)
+                    for (int u = 0; u < R; u++)
+                        (*tab)[off + j * R + u] = balanced(
+                            powmod_c(wb, static_cast<uint32_t>(j * u % L)));
+            }
+            off += (L + 3) & ~3;
+        }
+    }
+    if (tab)
+        tab->resize(off);
+    return off;
 }
 
-// columns per workgroup: a 64 KiB image (128 KiB at nmax = 2048)
-int lds_lgT(const qi_plan* p)
+size_t lds_bytes(const qi_plan* p, int lgT, int tw_words)
 {
-    const int lgn = ilog2i(p->nmax);
-    return std::min(6, std::max(4, 14 - lgn));
+    return ((static_cast<size_t>(p->nmax) << lgT) + lds_side_words(tw_words, p->k, p->len2k)) *
+           4;
+}
+
+constexpr size_t kLdsCap = 160 * 1024;  // LDS per CU
+
+// the table range [lo, hi) a mode stages (see the table order above)
+void lds_table_range(const qi_plan* p, int mode, int* lo, int* hi)
+{
+    XfPlan pl[4];
+    const int end = lds_tables(p, pl, nullptr);
+    if (mode == kLdsEnc) {
+        *lo = pl[kTwPnf].tw[0];
+        *hi = end;
+    } else {
+        *lo = 0;
+        *hi = mode == kLdsDec ? pl[kTwPnf].tw[0] : end;
+    }
+}
+
+// columns per workgroup: the widest tile (<= 64 columns) that leaves room
+// for two workgroups per CU, else for one (at least 8 columns)
+int lds_lgT(const qi_plan* p, int tw_words)
+{
+    for (int lg = 6; lg >= 3; lg--)
+        if (lds_bytes(p, lg, tw_words) <= kLdsCap / 2)
+            return lg;
+    return lds_bytes(p, 3, tw_words) <= kLdsCap ? 3 : -1;
+}
+
+bool lds_engine(const qi_plan* p)
+{
+    if (p->nmax > kLdsMaxN)
+        return false;
+    int lo, hi;
+    lds_table_range(p, kLdsSysDec, &lo, &hi);  // the largest set
+    return lds_lgT(p, hi - lo) >= 0;
 }
 
 int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
@@ -777,10 +851,22 @@ int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
     a.n = p->n;
     a.len2k = p->len2k;
     a.nmax = p->nmax;
-    a.lgT = lds_lgT(p);
-    a.pn = xf_plan(p->n);
-    a.p2k = xf_plan(p->len2k);
-    a.tw = p->d_tw[0];
+    XfPlan pl[4];
+    lds_tables(p, pl, nullptr);
+    int lo, hi;
+    lds_table_range(p, a.mode, &lo, &hi);
+    for (XfPlan& x : pl)
+        for (int q = 0; q < x.np; q++)
+            x.tw[q] -= lo;  // offsets within the staged range
+    a.pni = pl[kTwPni];
+    a.p2f = pl[kTwP2f];
+    a.p2i = pl[kTwP2i];
+    a.pnf = pl[kTwPnf];
+    a.tw = p->d_ldstw + lo;
+    a.tw_words = hi - lo;
+    a.lgT = lds_lgT(p, a.tw_words);
+    if (a.lgT < 0)
+        return -3;
     const NttCtxLayout L = ctx_layout_of(p);
     a.ids_off = static_cast<int>(L.ids_off());
     a.c_off = static_cast<int>(L.c_off());
@@ -789,8 +875,7 @@ int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
     if (tiles * S > 0x7fffffffLL)
         return -3;
     a.tiles = static_cast<int>(tiles);
-    const size_t lds = ((static_cast<size_t>(p->nmax) << a.lgT) +
-                        lds_side_words(p->nmax, p->k, p->len2k)) * 4;
+    const size_t lds = lds_bytes(p, a.lgT, a.tw_words);
     if (lds > 65536 &&
         hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_lds_kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -914,6 +999,15 @@ int ntt_plan_init(qi_plan* p)
     p->d_tw[1] = d + p->nmax;
     if (hipMemcpy(d, tw.data(), tw.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return -2;
+    if (lds_engine(p)) {
+        XfPlan pl[4];
+        std::vector<int32_t> tab;
+        lds_tables(p, pl, &tab);
+        if (hipMalloc(&p->d_ldstw, tab.size() * 4) != hipSuccess ||
+            hipMemcpy(p->d_ldstw, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) !=
+                hipSuccess)
+            return -2;
+    }
     if (p->sys) {
         // the systematic encode's constant context: points r^0 .. r^{k-1}
         const long long cs = ntt_ctx_words(p);
@@ -932,6 +1026,9 @@ void ntt_plan_free(qi_plan* p)
         (void)hipFree(p->d_tw[0]);
     if (p->d_sysctx)
         (void)hipFree(p->d_sysctx);
+    if (p->d_ldstw)
+        (void)hipFree(p->d_ldstw);
+    p->d_ldstw = nullptr;
     p->d_tw[0] = p->d_tw[1] = nullptr;
     p->d_sysctx = nullptr;
 }

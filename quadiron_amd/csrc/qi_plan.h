@@ -79,6 +79,7 @@ struct qi_plan {
     // encode's constant decode context
     int ntt = 0, len2k = 0, nmax = 0;
     int32_t* d_tw[2] = {nullptr, nullptr};
+    int32_t* d_ldstw = nullptr;  // per-pass twiddle tables of the LDS engine
     int32_t* d_sysctx = nullptr;
     uint32_t* d_err = nullptr;
     qi::HostState host;
