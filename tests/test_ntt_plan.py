@@ -1,0 +1,175 @@
+"""CPU: the index math of the general-path LDS engine (quadiron_amd/csrc/
+ntt.hip, ntt_lds_kernel), emulated in Python with exact modular arithmetic.
+
+The kernel runs forward transforms as decimation in frequency (natural order
+in, X[j] at pos(j) out) and inverse transforms as the transposed passes in
+reverse order (input at pos(t), natural order out), with per-pass twiddle
+tables laid out [j][u].  These tests mirror xf_plan / xf_pos / xf_index /
+lds_tables / lds_pass and check them against direct DFTs and against the
+decode pipeline of FecCode::decode_apply (reference src/fec_base.h:1418-1448):
+INTT_n -> NTT_2k -> x C -> INTT_2k.  The GPU parity tests then pin the
+kernel itself to the reference's golden vectors."""
+import random
+
+import pytest
+
+Q = 65537
+
+
+def root(n):
+    return pow(3, 65536 // n, Q)  # src/gf_ring.h:774-781 (primitive root 3)
+
+
+def xf_plan(N):
+    """ntt.hip xf_plan: radices <= 32, as even as possible; (lgr, sh) per
+    pass with s_q = N / (R_0 ... R_q) = 2^sh_q."""
+    bits = N.bit_length() - 1
+    np_ = max(1, (bits + 4) // 5)
+    lgr, sh, left, s = [], [], bits, bits
+    for q in range(np_):
+        b = (left + (np_ - q) - 1) // (np_ - q)
+        lgr.append(b)
+        s -= b
+        sh.append(s)
+        left -= b
+    return lgr, sh
+
+
+def xf_pos(plan, t):
+    lgr, sh = plan
+    p = 0
+    for b, s in zip(lgr, sh):
+        p += (t & ((1 << b) - 1)) << s
+        t >>= b
+    return p
+
+
+def xf_index(plan, p):
+    lgr, sh = plan
+    t, b0 = 0, 0
+    for b, s in zip(lgr, sh):
+        t += ((p >> s) & ((1 << b) - 1)) << b0
+        b0 += b
+    return t
+
+
+def tables(plan, nmax, inverse):
+    """lds_tables: pass q holds w_L^{+-j u} at j R + u (w_L = w_nmax^(nmax/L))."""
+    w = root(nmax)
+    out = []
+    for b, s in zip(*plan):
+        R, sq = 1 << b, 1 << s
+        L = R * sq
+        wl = pow(w, nmax // L, Q)
+        if inverse:
+            wl = pow(wl, Q - 2, Q)
+        out.append([pow(wl, (j * u) % L, Q) for j in range(sq) for u in range(R)])
+    return out
+
+
+def dft_r(v, inverse):
+    R = len(v)
+    wr = root(R)
+    o = [sum(v[t] * pow(wr, u * t, Q) for t in range(R)) % Q for u in range(R)]
+    return [o[(R - u) % R] for u in range(R)] if inverse else o
+
+
+def lds_transform(buf, N, plan, tabs, dif, inverse):
+    """lds_pass over every task, passes in order (DIF) or reversed (DIT)."""
+    lgr, sh = plan
+    order = range(len(lgr)) if dif else reversed(range(len(lgr)))
+    for q in order:
+        R, s = 1 << lgr[q], 1 << sh[q]
+        L = R * s
+        tw = tabs[q]
+        for tt in range(N // R):
+            j = tt & (s - 1)
+            base = (tt // s) * L + j
+            v = [buf[base + q2 * s] for q2 in range(R)]
+            w = tw[j * R:(j + 1) * R]
+            if not dif:
+                v = [v[i] * w[i] % Q for i in range(R)]
+            v = dft_r(v, inverse)
+            if dif:
+                v = [v[u] * w[u] % Q for u in range(R)]
+            for u in range(R):
+                buf[base + u * s] = v[u]
+
+
+@pytest.mark.parametrize("N", [2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048])
+def test_plan_shapes(N):
+    lgr, sh = xf_plan(N)
+    assert sum(lgr) == N.bit_length() - 1 and max(lgr) <= 5 and sh[-1] == 0
+    assert sorted(xf_pos((lgr, sh), t) for t in range(N)) == list(range(N))
+    assert all(xf_index((lgr, sh), xf_pos((lgr, sh), t)) == t for t in range(N))
+
+
+@pytest.mark.parametrize("N", [4, 32, 64, 256, 512])
+def test_dif_and_dit_orders(N):
+    rng = random.Random(N)
+    plan = xf_plan(N)
+    nmax = max(N, 512)
+    x = [rng.randrange(Q) for _ in range(N)]
+    w = root(N)
+    X = [sum(x[t] * pow(w, t * k, Q) for t in range(N)) % Q for k in range(N)]
+    wi = pow(w, Q - 2, Q)
+    Xi = [sum(x[t] * pow(wi, t * k, Q) for t in range(N)) % Q for k in range(N)]
+    b = list(x)  # DIF: natural in, X[j] at pos(j)
+    lds_transform(b, N, plan, tables(plan, nmax, False), True, False)
+    assert [b[xf_pos(plan, k)] for k in range(N)] == X
+    b = [0] * N  # inverse DIT: x[t] at pos(t), natural out
+    for t in range(N):
+        b[xf_pos(plan, t)] = x[t]
+    lds_transform(b, N, plan, tables(plan, nmax, True), False, True)
+    assert b == Xi
+
+
+def _ctx(k, n, len2k, ids):
+    """DecodeContext::init (src/fec_context.h:232-274): inv_A_i and
+    C[j] = -A(w_2k^j) / len_2k."""
+    r = root(n)
+    x = [pow(r, i, Q) for i in ids]
+    A = [1] + [0] * k
+    for xi in x:
+        A = [((A[d - 1] if d else 0) - xi * A[d]) % Q for d in range(k + 1)]
+    inv = []
+    for xi in x:
+        acc = 0
+        for d in range(k, 0, -1):
+            acc = (acc * xi + A[d] * d) % Q
+        inv.append(pow(acc * xi % Q, Q - 2, Q))
+    w2, il = root(len2k), pow(len2k, Q - 2, Q)
+    C = []
+    for j in range(len2k):
+        xj, acc = pow(w2, j, Q), 0
+        for d in range(k, -1, -1):
+            acc = (acc * xj + A[d]) % Q
+        C.append(-acc * il % Q)
+    return inv, C
+
+
+@pytest.mark.parametrize("k,m", [(65, 63), (100, 28), (40, 200)])
+def test_decode_pipeline(k, m):
+    """The kernel's decode order recovers the data polynomial's
+    coefficients from any k codeword symbols."""
+    rng = random.Random(k * m)
+    n = 1 << (k + m - 1).bit_length()
+    len2k = 1 << (2 * k - 1).bit_length()
+    nmax = max(n, len2k)
+    r = root(n)
+    coef = [rng.randrange(65536) for _ in range(k)]
+    cw = [sum(c * pow(r, i * t, Q) for t, c in enumerate(coef)) % Q for i in range(n)]
+    ids = sorted(rng.sample(range(k + m), k))
+    inv, C = _ctx(k, n, len2k, ids)
+    pn, p2 = xf_plan(n), xf_plan(len2k)
+    buf = [0] * nmax
+    for i, z in enumerate(ids):
+        buf[xf_pos(pn, z)] = cw[z] * inv[i] % Q
+    lds_transform(buf, n, pn, tables(pn, nmax, True), False, True)
+    for p in range(k, len2k):
+        buf[p] = 0
+    lds_transform(buf, len2k, p2, tables(p2, nmax, False), True, False)
+    for p in range(len2k):
+        buf[p] = buf[p] * C[xf_index(p2, p)] % Q
+    lds_transform(buf, len2k, p2, tables(p2, nmax, True), False, True)
+    assert buf[:k] == coef
