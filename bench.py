@@ -393,11 +393,14 @@ def main(argv=None):
     metric = ("device-resident encode+decode GB/s per GPU, RS-FNT k=16 n=64 "
               "pkt=64KiB" if headline else
               f"device-resident encode+decode GB/s per GPU, {name}")
+    # the plan's kernel choice (quadiron_amd/csrc/plan.cpp enc_matrix)
+    env_mat = os.environ.get("QI_ENC_MATRIX", "")
+    mat_enc = sys_ or (env_mat == "1" if env_mat in ("0", "1") else K == 64)
     if k > 64:
-        enc_kernel = "ntt_pass_kernel<*> (whole encode call)"
+        enc_kernel = "ntt_lds_kernel / ntt_pass_kernel (whole encode call)"
     else:
-        enc_kernel = (f"encode_fnt_kernel<{K},*>" if not sys_
-                      else "matrix_mfma_kernel<*>")
+        enc_kernel = ("matrix_mfma_kernel<*>" if mat_enc
+                      else f"encode_fnt_kernel<{K},*>")
     out = {
         "metric": metric,
         "value": value,

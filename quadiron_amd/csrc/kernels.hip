@@ -425,6 +425,10 @@ struct MatArgs {
     Oor in_oor;  // input marks (counts nullptr: none)
     int slot_base;
     Oor out_oor;  // output marks recorded (counts nullptr: none)
+    // output row of matrix row t (the plan groups a shared generator's
+    // row-scaled rows into as few 16-row blocks as possible); identity for
+    // decode matrices
+    const int32_t* rowmap;
     const uint32_t* route;
     long long rstride;
     SlowList slow;
@@ -468,7 +472,7 @@ __device__ __forceinline__ void push_slow_tile(const SlowList& sl, int s, long l
 __device__ void redo_marked_columns(const MatLayout& L, const int32_t* M,
                                                  const RowSrc& src, const RowDst& dst,
                                                  const OorScan& sc, long long col0,
-                                                 long long col1)
+                                                 long long col1, const int32_t* rowmap)
 {
     const int kin = L.kin;
     const int32_t* rscale = M + L.rscale();
@@ -519,7 +523,7 @@ __device__ void redo_marked_columns(const MatLayout& L, const int32_t* M,
                     y = static_cast<uint32_t>(
                         static_cast<uint64_t>(y) * static_cast<uint32_t>(rs < 0 ? rs + kQ : rs) %
                         65537u);
-                dst.base[sc.s * dst.ss + t * dst.rs + w] =
+                dst.base[sc.s * dst.ss + rowmap[t] * dst.rs + w] =
                     static_cast<uint16_t>(y == 65536u ? 0u : y);
             }
         }
@@ -566,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_st
             const long long col0 = static_cast<long long>(code >> 2) * 256;
             const long long col1 = col0 + (256LL << (code & 3));
             redo_marked_columns(L, mat + s * mat_stride, src, dst, sc, col0,
-                                col1 < words ? col1 : words);
+                                col1 < words ? col1 : words, a.rowmap);
         }
         __syncthreads();
         if (threadIdx.x == 0)
@@ -683,7 +687,8 @@ __device__ __forceinline__ void matrix_compute(
     const MatLayout& L, const int32_t* __restrict__ M,
     const int32_t (&xp)[COLS][KP], const Region<BUF>& go, uint32_t ors,
     uint32_t voff, long long col, long long col0, long long avail, int s,
-    int n_lm, const int* s_i, const uint32_t* s_col, const Oor& out_oor)
+    int n_lm, const int* s_i, const uint32_t* s_col, const Oor& out_oor,
+    const int32_t* __restrict__ rowmap)
 {
     // M: the per-stripe matrix block (wave-uniform: scalar loads)
     const int kin = L.kin;
@@ -742,11 +747,12 @@ __device__ __forceinline__ void matrix_compute(
             for (int c = 0; c < COLS; c++) {
                 if (static_cast<uint32_t>(y[c]) > 65535u && rec &&
                     (FULL || c < avail))
-                    record_oor(out_oor, s, t, col + c);
+                    record_oor(out_oor, s, rowmap[t], col + c);
                 o[c] = fix16(y[c]);
             }
         }
-        st<COLS, FULL, BUF, kAuxSt>(go, static_cast<uint32_t>(t) * ors, voff, avail, o);
+        st<COLS, FULL, BUF, kAuxSt>(go, static_cast<uint32_t>(rowmap[t]) * ors, voff, avail,
+                                    o);
     }
 }
 
@@ -849,11 +855,12 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(MatArgs a)
     const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
     if (full) {
         matrix_compute<KP, COLS, true, BUF>(L, M, xp, go, ors, voff, col, col0,
-                                            COLS, s, n_lm, s_i, s_col, out_oor);
+                                            COLS, s, n_lm, s_i, s_col, out_oor,
+                                            a.rowmap);
     } else if (col < words) {
         matrix_compute<KP, COLS, false, BUF>(L, M, xp, go, ors, voff, col, col0,
                                              words - col, s, n_lm, s_i, s_col,
-                                             out_oor);
+                                             out_oor, a.rowmap);
     }
     if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
         push_slow_tile(slow, s, col0, kBlock * COLS);
@@ -988,9 +995,10 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     const int RB = L.RB();
     const int32_t* mf = M + L.mf();
     const int32_t* kmf = M + L.kmf();
-    const int32_t* rscale = M + L.rscale();
+    const int32_t* rscale = M + L.rscale_mf();
     const int32_t* plain = M + L.plain();
-    auto load_ops = [&](int rb, qi_v2i (&b)[KS][3], int32_t& kt, int32_t& rs) {
+    const int32_t* __restrict__ rowmap = a.rowmap;
+    auto load_ops = [&](int rb, qi_v2i (&b)[KS][3], int32_t& kt, int32_t& rs, int32_t (&pr)[3]) {
 #pragma unroll
         for (int ks = 0; ks < KS; ks++)
 #pragma unroll
@@ -1004,6 +1012,13 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
         const int32_t k0 = kmf[tc], r0 = rscale[tc];
         kt = t < L.R ? k0 : 0;
         rs = t < L.R ? r0 : 1;
+        // output rows: this lane's epilogue row and its two store rows
+        pr[0] = rowmap[tc];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int ot = 16 * rb + 8 * h + (l >> 3);
+            pr[1 + h] = rowmap[ot < L.R ? ot : L.R - 1];
+        }
     };
     // tall matrices (RSPLIT, the encode generators): wave wv takes row
     // blocks wv, wv + NW, ... over all the block's super tiles, so each wave
@@ -1080,14 +1095,12 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     // One row block: every super tile's MFMAs, epilogue and stores, with
     // the block's operand tiles b / kt / rs.
     auto rb_body = [&](int rb, const qi_v2i (&bop)[KS][3], const int32_t kt,
-                       const int32_t rs) {
+                       const int32_t rs, const int32_t (&pr)[3]) {
         const int t = 16 * rb + tl;
         const bool trow = t < L.R;
         const int tcl = trow ? t : L.R - 1;  // a valid row for the loads
-#pragma unroll 1
-        for (int st = 0; st < nst; st++) {
-            const int ST = rsplit ? st : wv * nst + st;
-            qi_v4i acc[4][3];
+        // MFMAs of super tile ST into acc
+        auto tile_mfma = [&](const int ST, qi_v4i (&acc)[4][3]) {
 #pragma unroll
             for (int T = 0; T < 4; T++) {
                 acc[T][0] = qi_v4i{0, 0, 0, 0};
@@ -1132,6 +1145,9 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
                     }
                 }
             }
+        };
+        // epilogue + stores of super tile ST from its accumulators
+        auto tile_epi = [&](const int ST, qi_v4i (&acc)[4][3]) {
             // epilogue: lane (g, t) holds row t, columns cb .. cb + 15;
             // result j of chunk T is LDS byte 4 g + j = column 16 g + 4 T + j
             const long long cb = col0 + 64 * ST + 16 * g;
@@ -1164,10 +1180,11 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
                 }
             }
             if (__builtin_amdgcn_ballot_w64(rs != 1)) {
+                // every lane (rs = 1 keeps its value's residue: y is in
+                // [-1, 65536] either way): no per-element exec masking
 #pragma unroll
                 for (int c = 0; c < 16; c++)
-                    if (rs != 1)
-                        y[c] = fold(fold(mul_i24_s(y[c], rs)));
+                    y[c] = fold(fold(mul_i24_s(y[c], rs)));
             }
             uint32_t bad = 0;
 #pragma unroll
@@ -1178,7 +1195,7 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
                 for (int c = 0; c < 16; c++) {
                     if (static_cast<uint32_t>(y[c]) > 65535u) {
                         if (rec && trow)
-                            record_oor(out_oor, s, t, cb + c);
+                            record_oor(out_oor, s, pr[0], cb + c);
                         y[c] = 0;  // 65536 (or its alias -1) is stored as 0
                     }
                 }
@@ -1225,7 +1242,7 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
                 // so the compiler keeps an exact count of the stores in flight
                 const int ot = 16 * rb + orow;
                 const uint32_t vo =
-                    ot < L.R ? static_cast<uint32_t>(ot) * ors +
+                    ot < L.R ? static_cast<uint32_t>(pr[1 + h]) * ors +
                                    static_cast<uint32_t>((col0 + 64 * ST + 8 * c) * 2)
                              : 0x80000000u;
                 __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo), 0,
@@ -1235,6 +1252,33 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             // iteration's reads ahead of those writes
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
+        };
+        auto st_of = [&](int st) { return rsplit ? st : wv * nst + st; };
+        if constexpr (KS >= 2) {
+            // software pipeline: the next super tile's MFMAs are issued
+            // before this one's epilogue, so the matrix pipe runs under the
+            // epilogue's VALU work (two accumulator sets; KS >= 2 has the
+            // VGPRs, the LDS image already limits it to 2 waves per SIMD)
+            qi_v4i acc0[4][3], acc1[4][3];
+            tile_mfma(st_of(0), acc0);
+#pragma unroll 1
+            for (int st = 0; st < nst; st += 2) {
+                if (st + 1 < nst)
+                    tile_mfma(st_of(st + 1), acc1);
+                tile_epi(st_of(st), acc0);
+                if (st + 1 >= nst)
+                    break;
+                if (st + 2 < nst)
+                    tile_mfma(st_of(st + 2), acc0);
+                tile_epi(st_of(st + 1), acc1);
+            }
+        } else {
+#pragma unroll 1
+            for (int st = 0; st < nst; st++) {
+                qi_v4i acc[4][3];
+                tile_mfma(st_of(st), acc);
+                tile_epi(st_of(st), acc);
+            }
         }
     };
     // Row blocks in ping-pong over two operand buffers, each prefetch one row
@@ -1244,16 +1288,16 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     // every row block -- i.e. wait for all the previous block's streaming
     // stores before the next MFMA could issue.
     qi_v2i bA[KS][3], bB[KS][3];
-    int32_t ktA, rsA, ktB, rsB;
-    load_ops(rb0, bA, ktA, rsA);
+    int32_t ktA, rsA, ktB, rsB, prA[3], prB[3];
+    load_ops(rb0, bA, ktA, rsA, prA);
     const int rlast = RB - 1;
     for (int rb = rb0; rb < RB; rb += 2 * rbs) {
-        load_ops(min(rb + rbs, rlast), bB, ktB, rsB);
-        rb_body(rb, bA, ktA, rsA);
+        load_ops(min(rb + rbs, rlast), bB, ktB, rsB, prB);
+        rb_body(rb, bA, ktA, rsA, prA);
         if (rb + rbs >= RB)
             break;
-        load_ops(min(rb + 2 * rbs, rlast), bA, ktA, rsA);
-        rb_body(rb + rbs, bB, ktB, rsB);
+        load_ops(min(rb + 2 * rbs, rlast), bA, ktA, rsA, prA);
+        rb_body(rb + rbs, bB, ktB, rsB, prB);
     }
     if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
         push_slow_tile(slow, s, col0, NCOL);
@@ -1358,8 +1402,10 @@ __device__ void pack_row_g4(uint32_t* row, const MatLayout& L, int t,
         const uint32_t sq = sum % 65537u;
         block[L.kcorr() + t] = static_cast<int32_t>(mulm(sq, 32768u));
         block[L.rscale() + t] = s == 1 ? 1 : balanced(powm(s, 65535u));
-        if (L.KS())
+        if (L.KS()) {
             block[L.kmf() + t] = static_cast<int32_t>(mulm(sq, 32896u));
+            block[L.rscale_mf() + t] = block[L.rscale() + t];
+        }
     }
 }
 
@@ -1761,9 +1807,11 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
 int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
                   const int32_t* ids, long long is, RowSrc src, RowDst dst,
                   long long words, int S, const Oor* in_oor, int slot_base,
-                  const Oor* out_oor, const uint32_t* route, long long rstride,
-                  SlowList slow, uint32_t* err, hipStream_t st)
+                  const Oor* out_oor, const int32_t* rowmap, const uint32_t* route,
+                  long long rstride, SlowList slow, uint32_t* err, hipStream_t st)
 {
+    if (!rowmap)
+        return -1;
     if (L.KP != matrix_kp(L.kin))
         return -4;
     if (in_oor && !slow.base)
@@ -1773,7 +1821,7 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
               MatExt{extent(src.rows0, src.rs0, words), extent(src.rows1, src.rs1, words),
                      extent(L.R, dst.rs, words), 0},
               words, 0, in_oor ? *in_oor : none, slot_base, out_oor ? *out_oor : none,
-              route, rstride, in_oor ? slow : SlowList{nullptr, 0}, err};
+              rowmap, route, rstride, in_oor ? slow : SlowList{nullptr, 0}, err};
     const int rc = launch_matrix_kernels(a, S, st);
     if (rc || !in_oor)
         return rc;

@@ -20,6 +20,11 @@ namespace qi {
 //                  RB = ceil(R / 16) output blocks, KS = K-steps of 32
 //                  bytes, 3 operand types, 64 lanes x 8 bytes (pack_mf_dword)
 //   kmf[R]         32896 * sum_i c[t][i] mod q (undoes the byte offsets)
+//   rscale_mf[R]   the MFMA section's own inverse row scale: its tiles hold
+//                  the rows scaled for the i8 split alone (only 32640 is out
+//                  of its reach), so a shared generator's Vandermonde rows
+//                  that hit +-2^15 need no scale there (decode contexts use
+//                  one scale for both: rscale_mf = rscale)
 // The MFMA section exists (KS() > 0) when matrix_mfma_kernel takes the
 // block: kin <= 64.
 // A/B on MI355X, k = 16 decode: 1.54 ms on the matrix cores with the
@@ -45,7 +50,8 @@ struct MatLayout {
         return static_cast<size_t>(RB()) * KS() * 3 * 128;
     }
     QI_HD size_t kmf() const { return mf() + mf_words(); }
-    QI_HD size_t words() const { return kmf() + (KS() ? R : 0); }
+    QI_HD size_t rscale_mf() const { return kmf() + (KS() ? R : 0); }
+    QI_HD size_t words() const { return rscale_mf() + (KS() ? R : 0); }
 };
 
 QI_HD int32_t iabs32(int32_t v)
@@ -61,6 +67,12 @@ QI_HD int32_t iabs32(int32_t v)
 QI_HD bool coef_ok(int32_t c)
 {
     return iabs32(c) <= 32766 && c != 32640;
+}
+
+// Coefficients the i8 split alone can take (the matrix-core section).
+QI_HD bool coef_mf_ok(int32_t c)
+{
+    return c != 32640;
 }
 
 // c = 256 a + b (mod q) with a, b in [-128, 127], for a canonical c whose
@@ -117,8 +129,10 @@ QI_HD uint32_t pack_row(const uint32_t* row, const MatLayout& L, int t,
     const uint32_t sq = static_cast<uint32_t>(sum % 65537u);
     block[L.kcorr() + t] = static_cast<int32_t>(mulmod_c(sq, 32768u));
     block[L.rscale() + t] = s == 1 ? 1 : balanced(powmod_c(s, 65535u));
-    if (L.KS())
+    if (L.KS()) {
         block[L.kmf() + t] = static_cast<int32_t>(mulmod_c(sq, 32896u));
+        block[L.rscale_mf() + t] = block[L.rscale() + t];
+    }
     return s;
 }
 

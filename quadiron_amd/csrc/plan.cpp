@@ -1,6 +1,7 @@
 // Plan construction and host-side matrix math for the RS-FNT engine.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -14,12 +15,18 @@
 
 namespace qi {
 
-// QI_ENC_MATRIX=1 sends non-systematic encodes with K <= 64 through the
-// matrix-core kernel instead of the register FNT codelets (A/B knob)
-static bool enc_matrix_forced()
+// Non-systematic encodes with K <= 64 run the register FNT codelets, except
+// at K = 64, where the matrix-core kernel over the Vandermonde generator is
+// faster (cfg3: 1.04 vs 1.17 ms, profiles/r2_ab_enc_matrix.txt): a 64-point
+// codelet pass needs ~15.5 VALU per output, the MFMA epilogue ~6.  At
+// K = 16 (cfg2) the codelets win (3.65 vs 3.75 ms).  QI_ENC_MATRIX=1 / 0
+// forces either kernel (A/B and tests).
+static bool enc_matrix(int K)
 {
     const char* e = std::getenv("QI_ENC_MATRIX");
-    return e && e[0] == '1';
+    if (e && (e[0] == '0' || e[0] == '1'))
+        return e[0] == '1';
+    return K == 64;
 }
 
 static uint32_t addm(uint32_t a, uint32_t b)
@@ -72,13 +79,51 @@ std::vector<uint32_t> lagrange_matrix(int k, uint32_t r, const uint32_t* ids,
     return M;
 }
 
+// unit scale s for an MFMA row (s = 1 unless some entry is 32640), with
+// |s^-1| <= 32766 (the epilogue's y * s^-1 stays below 2^31)
+static uint32_t mf_row_scale(const uint32_t* row, int kin)
+{
+    for (uint32_t s = 1;; s++) {
+        const int32_t si = s == 1 ? 1 : balanced(powmod_c(s, 65535u));
+        if (iabs32(si) > 32766)
+            continue;
+        bool ok = true;
+        for (int i = 0; i < kin && ok; i++)
+            ok = coef_mf_ok(balanced(mulmod_c(row[i], s)));
+        if (ok)
+            return s;
+    }
+}
+
+bool mf_row_scaled(const uint32_t* row, int kin)
+{
+    return mf_row_scale(row, kin) != 1;
+}
+
 void pack_matrix(const MatLayout& L, const uint32_t* M, int32_t* block)
 {
     std::memset(block, 0, L.words() * sizeof(int32_t));
     for (int t = 0; t < L.R; t++)
         pack_row(M + static_cast<size_t>(t) * L.kin, L, t, block);
+    if (!L.KS())
+        return;
+    // the MFMA section from rows scaled for the i8 split alone
+    std::vector<int32_t> rows(static_cast<size_t>(L.R) * L.kin);
+    for (int t = 0; t < L.R; t++) {
+        const uint32_t* row = M + static_cast<size_t>(t) * L.kin;
+        const uint32_t s = mf_row_scale(row, L.kin);
+        uint64_t sum = 0;
+        for (int i = 0; i < L.kin; i++) {
+            const uint32_t c = mulmod_c(row[i], s);
+            rows[static_cast<size_t>(t) * L.kin + i] = static_cast<int32_t>(c);
+            sum += c;
+        }
+        block[L.kmf() + t] = static_cast<int32_t>(
+            mulmod_c(static_cast<uint32_t>(sum % 65537u), 32896u));
+        block[L.rscale_mf() + t] = s == 1 ? 1 : balanced(powmod_c(s, 65535u));
+    }
     for (size_t d = 0; d < L.mf_words(); d++)
-        block[L.mf() + d] = pack_mf_dword(L, block + L.plain(), d);
+        block[L.mf() + d] = pack_mf_dword(L, rows.data(), d);
 }
 
 }  // namespace qi
@@ -121,7 +166,7 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
         ok = ntt_plan_init(p) == 0;
     } else if (ok) {
         // twist factors w^{v t} for the encode passes (K <= 64)
-        if (!p->sys && !enc_matrix_forced()) {
+        if (!p->sys && !enc_matrix(p->K)) {
             const int passes = p->n / p->K;
             std::vector<int32_t> tw(static_cast<size_t>(passes) * p->K);
             for (int v = 0; v < passes; v++)
@@ -134,7 +179,7 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
         }
         // generator matrix for the systematic encode (and the matrix-core
         // A/B knob of the non-systematic one): outputs x inputs
-        if (ok && (p->sys || enc_matrix_forced())) {
+        if (ok && (p->sys || enc_matrix(p->K))) {
             const int kp = matrix_kp(k);
             MatLayout L{p->n_outputs, k, kp};
             std::vector<uint32_t> M;
@@ -154,13 +199,38 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
                         M[static_cast<size_t>(i) * k + t] = powmod_c(
                             p->r, static_cast<uint32_t>((static_cast<long long>(i) * t) % p->n));
             }
+            // rows whose matrix-core tiles need a unit scale (an entry of
+            // 32640, the one residue the i8 split cannot reach) go last:
+            // the epilogue multiplies back by the scale for a whole 16-row
+            // block when any of its rows needs it.  Vandermonde rows hit
+            // 32640 (a root of unity) often: at cfg3, 160 of 1024 rows,
+            // spread over 52 of the 64 blocks in natural order, 10 after.
+            const int R = p->n_outputs;
+            std::vector<int32_t> perm;
+            for (int pass = 0; pass < 2; pass++)
+                for (int i = 0; i < R; i++)
+                    if (mf_row_scaled(M.data() + static_cast<size_t>(i) * k, k) == (pass == 1))
+                        perm.push_back(i);
+            std::vector<uint32_t> Mp(M.size());
+            for (int i = 0; i < R; i++)
+                std::copy_n(M.begin() + static_cast<size_t>(perm[i]) * k, k,
+                            Mp.begin() + static_cast<size_t>(i) * k);
             std::vector<int32_t> blk(L.words());
-            pack_matrix(L, M.data(), blk.data());
+            pack_matrix(L, Mp.data(), blk.data());
             p->gen = L;
             ok = hipMalloc(&p->d_gen, blk.size() * 4) == hipSuccess &&
                  hipMemcpy(p->d_gen, blk.data(), blk.size() * 4, hipMemcpyHostToDevice) ==
+                     hipSuccess &&
+                 hipMalloc(&p->d_rowmap, perm.size() * 4) == hipSuccess &&
+                 hipMemcpy(p->d_rowmap, perm.data(), perm.size() * 4, hipMemcpyHostToDevice) ==
                      hipSuccess;
         }
+        // identity output rows of the k x k decode matrices
+        std::vector<int32_t> id(k);
+        for (int i = 0; i < k; i++)
+            id[i] = i;
+        ok = ok && hipMalloc(&p->d_rowid, id.size() * 4) == hipSuccess &&
+             hipMemcpy(p->d_rowid, id.data(), id.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
     }
     if (!ok) {
         qi_plan_destroy(p);
@@ -177,6 +247,10 @@ void qi_plan_destroy(qi_plan* p)
         (void)hipFree(p->d_twist);
     if (p->d_gen)
         (void)hipFree(p->d_gen);
+    if (p->d_rowmap)
+        (void)hipFree(p->d_rowmap);
+    if (p->d_rowid)
+        (void)hipFree(p->d_rowid);
     if (p->d_err)
         (void)hipFree(p->d_err);
     ntt_plan_free(p);

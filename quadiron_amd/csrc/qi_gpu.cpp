@@ -100,7 +100,7 @@ int qi_gpu_encode(qi_plan* p, const uint16_t* d_data, long long dss,
                                  p->d_err, st(stream));
     RowSrc src{d_data, dss, drs, 1 << 30, nullptr, 0, 0, 0, p->k, 0};
     return launch_matrix(p->gen, p->d_gen, 0, nullptr, 0, src, out, words,
-                         n_stripes, nullptr, 0, d_counts ? &oor : nullptr,
+                         n_stripes, nullptr, 0, d_counts ? &oor : nullptr, p->d_rowmap,
                          nullptr, 0, SlowList{nullptr, 0}, p->d_err, st(stream));
 }
 
@@ -156,7 +156,7 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
                           words, n_stripes, st(stream));
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, p->sys ? p->k : 0,
-                         nullptr,
+                         nullptr, p->d_rowid,
                          reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
                          cs, ctx_slow(p, d_ctx, words), p->d_err, st(stream));
 }
@@ -196,7 +196,7 @@ int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
         return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, 0, out, words,
                           n_stripes, st(stream));
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
-                         n_stripes, d_counts ? &in : nullptr, 0, nullptr,
+                         n_stripes, d_counts ? &in : nullptr, 0, nullptr, p->d_rowid,
                          reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
                          cs, ctx_slow(p, d_ctx, words), p->d_err, st(stream));
 }

@@ -89,13 +89,15 @@ int launch_encode_fnt(int k, int n, int n_out, const int32_t* d_twist,
 //   in_oor: restore buckets by slot (nullptr = none); slot_of_id = id -
 //     slot_base (ids < slot_base have no bucket)
 //   out_oor: record OOR outputs (nullptr = no recording; values stored as 0)
+//   rowmap: output row (and OOR slot) of matrix row t (R entries, required;
+//   identity for decode matrices)
 //   route: per-stripe OOR routing tables (route_stride u32 apart), or null
 //   slow: per-stripe slow-tile lists (required when in_oor is given)
 int launch_matrix(const MatLayout& L, const int32_t* mat, long long mat_stride,
                   const int32_t* ids, long long ids_stride, RowSrc src,
                   RowDst dst, long long words,
                   int n_stripes, const Oor* in_oor, int slot_base,
-                  const Oor* out_oor, const uint32_t* route,
+                  const Oor* out_oor, const int32_t* rowmap, const uint32_t* route,
                   long long route_stride, SlowList slow, uint32_t* d_err,
                   hipStream_t stream);
 

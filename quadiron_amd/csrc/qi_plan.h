@@ -74,6 +74,11 @@ struct qi_plan {
     int32_t* d_twist = nullptr;  // encode twist factors (non-systematic)
     int32_t* d_gen = nullptr;    // generator matrix block (matrix encode)
     qi::MatLayout gen{0, 0, 0};
+    // output row of each generator row (rows needing a unit scale grouped
+    // at the end, so few 16-row blocks run the scaling epilogue), and the
+    // identity map of the k x k decode matrices
+    int32_t* d_rowmap = nullptr;
+    int32_t* d_rowid = nullptr;
     // general-k path (k > 64, ntt.hip): transforms of length <= nmax =
     // max(n, len_2k), balanced twiddle tables w^e / w^-e, and the systematic
     // encode's constant decode context

@@ -303,9 +303,21 @@ def test_general_path_slicing(k, m, sys_, S, P):
 ])
 def test_matrix_encode_knob_vs_oracle(monkeypatch, k, m, S, P):
     """QI_ENC_MATRIX=1 (read at plan creation) sends non-systematic encodes
-    through the matrix-core kernel: the A/B path must stay bit-exact too."""
+    through the matrix-core kernel (the default at K = 64 only): bit-exact
+    on every generator shape, including the permuted rows of the cfg3
+    Vandermonde generator."""
     monkeypatch.setenv("QI_ENC_MATRIX", "1")
     _batch_roundtrip(k, m, 0, S, P, seed=7 * k + m + P, n_craft=16)
+
+
+@pytest.mark.parametrize("k,m,S,P", [
+    (64, 960, 2, 2048),       # cfg3 shape: the 64-point codelet kernel
+    (33, 31, 2, 513),
+])
+def test_codelet_encode_knob_vs_oracle(monkeypatch, k, m, S, P):
+    """QI_ENC_MATRIX=0 keeps the register FNT codelets at K = 64 too."""
+    monkeypatch.setenv("QI_ENC_MATRIX", "0")
+    _batch_roundtrip(k, m, 0, S, P, seed=11 * k + m + P, n_craft=16)
 
 
 def test_cfg2_full_size_roundtrip():
