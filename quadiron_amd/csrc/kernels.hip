@@ -1254,31 +1254,15 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             __builtin_amdgcn_wave_barrier();
         };
         auto st_of = [&](int st) { return rsplit ? st : wv * nst + st; };
-        if constexpr (KS >= 2) {
-            // software pipeline: the next super tile's MFMAs are issued
-            // before this one's epilogue, so the matrix pipe runs under the
-            // epilogue's VALU work (two accumulator sets; KS >= 2 has the
-            // VGPRs, the LDS image already limits it to 2 waves per SIMD)
-            qi_v4i acc0[4][3], acc1[4][3];
-            tile_mfma(st_of(0), acc0);
+        // (issuing the next super tile's MFMAs ahead of this epilogue, with
+        // a second accumulator set, measured no gain at KS = 2 or 4:
+        // profiles/r2_ab_pipe.txt)
 #pragma unroll 1
-            for (int st = 0; st < nst; st += 2) {
-                if (st + 1 < nst)
-                    tile_mfma(st_of(st + 1), acc1);
-                tile_epi(st_of(st), acc0);
-                if (st + 1 >= nst)
-                    break;
-                if (st + 2 < nst)
-                    tile_mfma(st_of(st + 2), acc0);
-                tile_epi(st_of(st + 1), acc1);
-            }
-        } else {
-#pragma unroll 1
-            for (int st = 0; st < nst; st++) {
-                qi_v4i acc[4][3];
-                tile_mfma(st_of(st), acc);
-                tile_epi(st_of(st), acc);
-            }
+        for (int st = 0; st < nst; st++) {
+            qi_v4i acc[4][3];
+            tile_mfma(st_of(st), acc);
+            tile_epi(st_of(st), acc);
+        }
         }
     };
     // Row blocks in ping-pong over two operand buffers, each prefetch one row
