@@ -1263,7 +1263,6 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             tile_mfma(st_of(st), acc);
             tile_epi(st_of(st), acc);
         }
-        }
     };
     // Row blocks in ping-pong over two operand buffers, each prefetch one row
     // block ahead and unconditional (a clamped row block past the end).  On
