@@ -1653,9 +1653,7 @@ int matrix_kp(int kin)
         return 16;
     if (pairs <= 32)
         return 32;
-    if (pairs <= 64)
-        return 64;
-    return -1;
+    return -1;  // k > 64 runs the NTT path (ntt.hip)
 }
 
 template <int KP, int COLS, bool BUF>
@@ -1780,8 +1778,6 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
         return mat_dispatch<16>(cols, a, S, st);
     case 32:
         return mat_dispatch<32>(cols, a, S, st);
-    case 64:
-        return mat_dispatch<64>(cols, a, S, st);
     default:
         return -3;
     }
