@@ -1300,11 +1300,15 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
 // 2^32 = 1, p = p0 + p1 2^16 + p2 2^32 reduces to p0 - p1 + p2
 __device__ __forceinline__ uint32_t mulm(uint32_t a, uint32_t b)
 {
-    const uint64_t p = static_cast<uint64_t>(a) * b;
-    const int32_t v = static_cast<int32_t>(p & 0xffffu) -
-                      static_cast<int32_t>((p >> 16) & 0xffffu) +
-                      static_cast<int32_t>(p >> 32);  // [-65535, 65536]
-    return static_cast<uint32_t>(v < 0 ? v + 65537 : v);
+    // balanced operands (|a|, |b| <= 32768): the product fits int32 and one
+    // full-rate v_mul_i32_i24 forms it (the 64-bit product took two
+    // quarter-rate v_mul_{lo,hi}_u32 on the serial Lagrange chains)
+    const int32_t ab = static_cast<int32_t>(a) - (a > 32768u ? 65537 : 0);
+    const int32_t bb = static_cast<int32_t>(b) - (b > 32768u ? 65537 : 0);
+    const int32_t p = __mul24(ab, bb);                      // |p| <= 2^30
+    const int32_t v = (p & 0xffff) - (p >> 16);             // [-16384, 81919]
+    const int32_t w = v < 0 ? v + 65537 : v;                // [0, 81919]
+    return static_cast<uint32_t>(w >= 65537 ? w - 65537 : w);
 }
 __device__ __forceinline__ uint32_t addm(uint32_t a, uint32_t b)
 {
@@ -1328,29 +1332,37 @@ __device__ __forceinline__ uint32_t powm(uint32_t b, uint32_t e)
 
 // NT threads: the Lagrange part runs on the first wave (lane = point); the
 // row packing and the MFMA operand tiles use every thread (NT = 256 for
-// k > 32, where they dominate and there are few stripes per launch)
-// pack_row (matrix_pack.h) on a group of 4 adjacent lanes, lane `sub`
-// taking entries sub, sub + 4, ...: the same row scale search (uniform in
-// the group), packed pairs, canonical `plain` entries, kcorr / rscale / kmf,
-// and the row-scaled entries written back to the LDS row for the tiles
-__device__ __forceinline__ uint32_t g4_or(uint32_t v)
+// k > 32, where they dominate and there are few stripes per launch).
+// pack_row (matrix_pack.h) on a group of LPR adjacent lanes (a power of 2,
+// <= 16), lane `sub` taking entries sub, sub + LPR, ...: the column scale
+// 1 / A'(x_i) applied, the same row scale search (uniform in the group),
+// packed pairs, canonical `plain` entries, kcorr / rscale / kmf, and the
+// row-scaled entries written back to the LDS row for the tiles.  Entries
+// lane-fastest: a group's global stores are runs of LPR dwords (4 lanes per
+// row with 16-byte runs took 17 of the 43 us of a k = 64 context).
+__device__ __forceinline__ uint32_t grp_or(uint32_t v, int lpr)
 {
-    v |= __shfl_xor(v, 1, 4);
-    return v | __shfl_xor(v, 2, 4);
+    for (int m = 1; m < lpr; m <<= 1)
+        v |= __shfl_xor(v, m, lpr);
+    return v;
 }
-__device__ __forceinline__ uint32_t g4_add(uint32_t v)
+__device__ __forceinline__ uint32_t grp_add(uint32_t v, int lpr)
 {
-    v += __shfl_xor(v, 1, 4);
-    return v + __shfl_xor(v, 2, 4);
+    for (int m = 1; m < lpr; m <<= 1)
+        v += __shfl_xor(v, m, lpr);
+    return v;
 }
-__device__ void pack_row_g4(uint32_t* row, const MatLayout& L, int t,
-                            int32_t* block, int sub)
+__device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLayout& L,
+                             int t, int32_t* block, int sub, int lpr)
 {
     const int kin = L.kin, KP = L.KP;
     uint32_t bad = 0;
-    for (int i = sub; i < kin; i += 4)
-        bad |= !coef_ok(balanced(row[i]));
-    bad = g4_or(bad);
+    for (int i = sub; i < kin; i += lpr) {
+        const uint32_t c = mulm(row[i], cscale[i]);
+        row[i] = c;
+        bad |= !coef_ok(balanced(c));
+    }
+    bad = grp_or(bad, lpr);
     uint32_t s = 1;
     while (bad) {  // rare; s, si and bad are uniform in the group
         s++;
@@ -1358,31 +1370,33 @@ __device__ void pack_row_g4(uint32_t* row, const MatLayout& L, int t,
         if (iabs32(si) > 32766)
             continue;
         bad = 0;
-        for (int i = sub; i < kin; i += 4)
+        for (int i = sub; i < kin; i += lpr)
             bad |= !coef_ok(balanced(mulm(row[i], s)));
-        bad = g4_or(bad);
+        bad = grp_or(bad, lpr);
+    }
+    if (s != 1) {  // every lane of the group reads only its own entries
+        for (int i = sub; i < kin; i += lpr)
+            row[i] = mulm(row[i], s);
     }
     int32_t* packed = block + static_cast<size_t>(t) * KP;
     int32_t* plain = block + L.plain();
-    for (int j = sub; j < KP; j += 4) {
-        int32_t lo = 0, hi = 0;
-        if (2 * j < kin)
-            lo = balanced(s == 1 ? row[2 * j] : mulm(row[2 * j], s));
-        if (2 * j + 1 < kin)
-            hi = balanced(s == 1 ? row[2 * j + 1] : mulm(row[2 * j + 1], s));
+    for (int j = sub; j < KP; j += lpr) {
+        const int32_t lo = 2 * j < kin ? balanced(row[2 * j]) : 0;
+        const int32_t hi = 2 * j + 1 < kin ? balanced(row[2 * j + 1]) : 0;
         packed[j] = static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xffffu) |
                                          (static_cast<uint32_t>(hi) << 16));
     }
-    uint32_t sum = 0;  // <= 64 * 65536
-    for (int i = sub; i < kin; i += 4) {
-        const uint32_t c = s == 1 ? row[i] : mulm(row[i], s);
+    uint32_t sum = 0;  // <= 64 * 65536 < 2^23
+    for (int i = sub; i < kin; i += lpr) {
+        const uint32_t c = row[i];
         plain[static_cast<size_t>(t) * kin + i] = static_cast<int32_t>(c);
-        row[i] = c;
         sum += c;
     }
-    sum = g4_add(sum);
+    sum = grp_add(sum, lpr);
     if (sub == 0) {
-        const uint32_t sq = sum % 65537u;
+        // sum mod q by one fold (2^16 = -1): [-127, 65535] -> canonical
+        const int32_t f = static_cast<int32_t>(sum & 0xffffu) - static_cast<int32_t>(sum >> 16);
+        const uint32_t sq = static_cast<uint32_t>(f < 0 ? f + 65537 : f);
         block[L.kcorr() + t] = static_cast<int32_t>(mulm(sq, 32768u));
         block[L.rscale() + t] = s == 1 ? 1 : balanced(powm(s, 65535u));
         if (L.KS()) {
@@ -1390,6 +1404,12 @@ __device__ void pack_row_g4(uint32_t* row, const MatLayout& L, int t,
             block[L.rscale_mf() + t] = block[L.rscale() + t];
         }
     }
+}
+
+// LDS row pitch of the context kernel's k x k matrix: 4 x odd, >= k
+__host__ __device__ inline int ctx_pitch(int k)
+{
+    return (k + 3) / 8 * 8 + 4;
 }
 
 template <int NT>
@@ -1400,13 +1420,16 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
 {
     __shared__ uint32_t xs[64];
     __shared__ uint32_t A[65];
+    __shared__ uint32_t cinv[64];  // 1 / A'(x_i)
     // k x k matrix (and the Q_i coefficients in systematic mode), sized by
     // the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
     // limited the kernel to 4 workgroups per CU
-    extern __shared__ uint32_t qi_ctx_lds[];
-    // rows at an odd pitch: the 4-lanes-per-row passes below read 16 rows
-    // per wave, which a pitch of k (a power of two) put in one LDS bank
-    const int kp = k | 1;
+    extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
+    // row pitch = 4 x odd (>= k, a multiple of 4 words): the tile pass
+    // reads 16 rows x 16 bytes per wave (ds_read_b128) conflict-free (the
+    // odd pitch k | 1 had SQ_LDS_BANK_CONFLICT at 7.4 cycles per LDS
+    // instruction at k = 64)
+    const int kp = ctx_pitch(k);
     uint32_t* Mt = qi_ctx_lds;
     uint32_t* Qt = qi_ctx_lds + k * kp;
     const int s = blockIdx.x;
@@ -1467,72 +1490,82 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     }
     __syncthreads();
     if (tid < k) {
-        // 1 / A'(x_i) = 1 / prod_{j != i} (x_i - x_j)
+        // Q_i = A / (x - x_i) by synthetic division from the top, and
+        // A'(x_i) = Q_i(x_i) by Horner over the same coefficients (two
+        // interleaved chains; the product prod_{j != i} (x_i - x_j) was a
+        // third serial chain).  The rows hold the unscaled values; the
+        // column scale 1 / A'(x_i) is applied by the packing pass.
         const uint32_t xi = xs[tid];
-        uint32_t den = 1;
-        for (int j = 0; j < k; j++)
-            if (j != tid)
-                den = mulm(den, subm(xi, xs[j]));
-        const uint32_t inv = powm(den, 65535u);
-        // Q_i = A / (x - x_i) by synthetic division from the top
-        uint32_t q = 1;  // A[k]
+        uint32_t q = 1, h = 1;  // A[k]; Q_i(x_i) so far
         uint32_t* dst = mode == 0 ? Mt : Qt;
-        const uint32_t sc = mode == 0 ? inv : 1u;
-        dst[(k - 1) * kp + tid] = sc;
+        dst[(k - 1) * kp + tid] = 1;
         for (int j = k - 1; j >= 1; j--) {
             q = addm(A[j], mulm(xi, q));
-            dst[(j - 1) * kp + tid] = mulm(q, sc);
+            dst[(j - 1) * kp + tid] = q;
+            h = addm(mulm(h, xi), q);
         }
+        cinv[tid] = powm(h, 65535u);
         if (mode != 0) {
-            // M[t][i] = Q_i(r^t) / A'(x_i)
+            // M[t][i] = Q_i(r^t) (/ A'(x_i) in the packing pass)
             uint32_t e = 1;
             for (int t = 0; t < k; t++) {
                 uint32_t acc = 0;
                 for (int j = k - 1; j >= 0; j--)
                     acc = addm(mulm(acc, e), Qt[j * kp + tid]);
-                Mt[t * kp + tid] = mulm(acc, inv);
+                Mt[t * kp + tid] = acc;
                 e = mulm(e, r);
             }
         }
     }
     __syncthreads();
-    // 4 lanes per row: pack_row's work split over the row's entries, its
-    // reductions over the 4 lanes (k = 64: 92 -> 62 us per 1024 stripes)
-    for (int t = tid / 4; t < L.R; t += NT / 4)
-        pack_row_g4(Mt + t * kp, L, t, mat, tid & 3);
+    {
+        // LPR lanes per row: 4 entries per lane at k = 64
+        const int q4 = (k + 3) / 4;
+        const int lpr = q4 <= 4 ? 4 : q4 <= 8 ? 8 : 16;
+        for (int t = tid / lpr; t < L.R; t += NT / lpr)
+            pack_row_grp(Mt + t * kp, cinv, L, t, mat, tid & (lpr - 1), lpr);
+    }
     if (L.KS()) {
         // the matrix-core operand tiles, from the row-scaled entries in LDS
         __syncthreads();
-        const int32_t* rows = reinterpret_cast<const int32_t*>(Mt);
         // per (row t, 4 consecutive entries): split once, then place the
-        // a / b byte words in their 6 tile dwords (pack_mf_dword's layout,
-        // zeros included; rows t >= R are zero)
-        const int KS = L.KS(), KH = 16 * KS, RBp = L.RB() * 16;
+        // a / b byte words in their tile dwords (pack_mf_dword's layout;
+        // rows t >= R are zero).  Items run row-fastest, so 16 lanes read
+        // 16 rows' entries i0..i0+3 (one ds_read_b128 each) and a wave's
+        // stores cover whole 128-byte tile lines (16 rows x 2 dwords).  At
+        // KS = 4 the zero halves of [a | 0] and [0 | b] are not written:
+        // matrix_mfma_kernel skips those K-steps (and never loads them).
+        const int KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
         int32_t* mf = mat + L.mf();
-        for (int it = tid; it < RBp * (KH / 4); it += NT) {
-            const int t = it / (KH / 4), i0 = 4 * (it % (KH / 4));
+        for (int it = tid; it < RB * nj * 16; it += NT) {
+            const int tl4 = it & 15, jj = it >> 4;
+            const int j = jj % nj, rb = jj / nj;
+            const int t = 16 * rb + tl4, i0 = 4 * j;
             uint32_t aw = 0, bw = 0;
-            if (t < L.R) {
+            if (t < L.R && i0 < k) {
+                const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
+                const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
 #pragma unroll
                 for (int jb = 0; jb < 4; jb++) {
                     if (i0 + jb < k) {
                         int32_t a, b;
-                        split_i8(static_cast<uint32_t>(rows[t * kp + i0 + jb]), a, b);
+                        split_i8(e[jb], a, b);
                         aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
                         bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
                     }
                 }
             }
-            const int rb = t >> 4, tl4 = t & 15;
 #pragma unroll
             for (int half = 0; half < 2; half++) {
                 const int K = half * KH + i0;
                 const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
                 const size_t base =
                     static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl4) * 2 + dw;
-                mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
-                mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
-                mf[base + 256] = static_cast<int32_t>(half ? aw : bw);  // [b | a]
+                if (KS != 4 || half == 0)
+                    mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
+                if (KS != 4 || half == 1)
+                    mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
+                mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
             }
         }
     }
@@ -1818,7 +1851,7 @@ int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
     if (k > 64 || S <= 0)
         return -3;
     Oor none{nullptr, nullptr, 0, 0};
-    const size_t lds = static_cast<size_t>(k) * (k | 1) * 4 * (mode ? 2 : 1);
+    const size_t lds = static_cast<size_t>(k) * ctx_pitch(k) * 4 * (mode ? 2 : 1);
     if (k > 32)
         hipLaunchKernelGGL(decode_ctx_kernel<256>, dim3(S), dim3(256), lds, st, k, r,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,

@@ -174,7 +174,10 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
     for s in range(S):
         ids[s] = np.sort(rng.choice(k + m, k, replace=False))
     di = torch.from_numpy(ids.view(np.int16)).cuda()
-    ctx = torch.zeros(plan.ctx_bytes(S, P), dtype=torch.uint8, device="cuda")
+    # a context buffer full of garbage: the context kernel must write every
+    # word the decode reads (it skips the tiles' zero halves at k > 32)
+    ctx = torch.randint(0, 256, (plan.ctx_bytes(S, P),), dtype=torch.uint8,
+                        device="cuda")
     plan.decode_ctx(di, ctx, P, counts, entries, cap, h_ids=ids)
     dec = torch.zeros((S, k, P), dtype=torch.int16, device="cuda")
     err = plan.decode(ctx, di, out, dec, data=dd, counts=counts,
@@ -198,7 +201,7 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
     recv = torch.gather(full, 1, idx[:, :, None].expand(S, k, P)).contiguous()
     pcnt = torch.gather(fcnt, 1, idx).contiguous()
     pent = torch.gather(fent, 1, idx[:, :, None].expand(S, k, cap)).contiguous()
-    ctx2 = torch.zeros_like(ctx)
+    ctx2 = torch.full_like(ctx, 0xA5)
     plan.decode_ctx_packed(di, ctx2, P, pcnt, pent, cap, h_ids=ids)
     dec2 = torch.zeros_like(dec)
     assert plan.decode_packed(ctx2, recv, dec2, pcnt, pent, cap) == 0
