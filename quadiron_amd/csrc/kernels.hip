@@ -1272,8 +1272,8 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     // stores before the next MFMA could issue.
     qi_v2i bA[KS][3], bB[KS][3];
     int32_t ktA, rsA, ktB, rsB, prA[3], prB[3];
-    load_ops(rb0, bA, ktA, rsA, prA);
     const int rlast = RB - 1;
+    load_ops(min(rb0, rlast), bA, ktA, rsA, prA);
     for (int rb = rb0; rb < RB; rb += 2 * rbs) {
         load_ops(min(rb + rbs, rlast), bB, ktB, rsB, prB);
         rb_body(rb, bA, ktA, rsA, prA);
@@ -1294,7 +1294,7 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
 //   mode 1: M[t][i] = Q_i(r^t)   / A'(x_i)        (systematic)
 // plus the OOR route table of the stripe (decode_prepare's props walk,
 // src/fec_base.h:1361-1404, precomputed per tile).
-// One 64-lane workgroup per stripe; k <= 64.
+// One workgroup per stripe (64 lanes for k <= 32, else 256); k <= 128.
 // ---------------------------------------------------------------------------
 // canonical a * b mod 65537 for a, b in [0, 65536]: with 2^16 = -1 and
 // 2^32 = 1, p = p0 + p1 2^16 + p2 2^32 reduces to p0 - p1 + p2
@@ -1418,9 +1418,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
     int by_pos, long long words, uint32_t* err)
 {
-    __shared__ uint32_t xs[64];
-    __shared__ uint32_t A[65];
-    __shared__ uint32_t cinv[64];  // 1 / A'(x_i)
+    __shared__ uint32_t xs[128];
+    __shared__ uint32_t A[129];
+    __shared__ uint32_t cinv[128];  // 1 / A'(x_i)
     // k x k matrix (and the Q_i coefficients in systematic mode), sized by
     // the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
     // limited the kernel to 4 workgroups per CU
@@ -1474,15 +1474,31 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             }
         }
     }
-    // A(x) = prod_i (x - x_i), lane d holding coefficient d (A is monic:
-    // A[k] = 1 is set explicitly, so k = 64 needs no 65th lane)
+    // A(x) = prod_i (x - x_i), lane d holding coefficient d (and d + 64
+    // for k > 64).  A is monic: A[k] = 1 is set explicitly, so k = 64 (128)
+    // needs no 65th (129th) coefficient slot.
     if (tid < 64) {  // wave 0 (wave-uniform)
         uint32_t a = tid == 0 ? 1u : 0u;
-        for (int i = 0; i < k; i++) {
-            uint32_t prev = __shfl_up(a, 1);
-            if (tid == 0)
-                prev = 0;
-            a = subm(prev, mulm(xs[i], a));
+        if (k <= 64) {
+            for (int i = 0; i < k; i++) {
+                uint32_t prev = __shfl_up(a, 1);
+                if (tid == 0)
+                    prev = 0;
+                a = subm(prev, mulm(xs[i], a));
+            }
+        } else {
+            uint32_t a1 = 0;
+            for (int i = 0; i < k; i++) {
+                uint32_t prev = __shfl_up(a, 1), prev1 = __shfl_up(a1, 1);
+                const uint32_t top = __shfl(a, 63);  // coefficient 63 -> 64
+                if (tid == 0) {
+                    prev = 0;
+                    prev1 = top;
+                }
+                a = subm(prev, mulm(xs[i], a));
+                a1 = subm(prev1, mulm(xs[i], a1));
+            }
+            A[64 + tid] = a1;
         }
         A[tid] = a;
         if (tid == 0)
@@ -1533,7 +1549,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         // rows t >= R are zero).  Items run row-fastest, so 16 lanes read
         // 16 rows' entries i0..i0+3 (one ds_read_b128 each) and a wave's
         // stores cover whole 128-byte tile lines (16 rows x 2 dwords).  At
-        // KS = 4 the zero halves of [a | 0] and [0 | b] are not written:
+        // KS >= 4 the zero halves of [a | 0] and [0 | b] are not written:
         // matrix_mfma_kernel skips those K-steps (and never loads them).
         const int KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
         int32_t* mf = mat + L.mf();
@@ -1561,9 +1577,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                 const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
                 const size_t base =
                     static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl4) * 2 + dw;
-                if (KS != 4 || half == 0)
+                if (KS < 4 || half == 0)
                     mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
-                if (KS != 4 || half == 1)
+                if (KS < 4 || half == 1)
                     mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
                 mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
             }
@@ -1686,7 +1702,9 @@ int matrix_kp(int kin)
         return 16;
     if (pairs <= 32)
         return 32;
-    return -1;  // k > 64 runs the NTT path (ntt.hip)
+    if (pairs <= 64)
+        return 64;
+    return -1;  // k > 128 runs the NTT path (ntt.hip)
 }
 
 template <int KP, int COLS, bool BUF>
@@ -1763,9 +1781,17 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
 {
     constexpr int NSTS = KS == 1 ? 16 : 8;
     const int RB = a.L.RB();
-    if (RB >= 4)
-        return mfma_launch<KS, NSTS, 4, true>(a, wfull, S, st);
-    return mfma_launch<KS, NSTS, 4, false>(a, wfull, S, st);
+    if constexpr (KS == 8) {
+        // 65 <= k <= 128: 128 columns (a 256-row byte-plane image, 37 KB),
+        // the waves always splitting the row blocks (a wave past the last
+        // row block idles)
+        (void)RB;
+        return mfma_launch<KS, 2, 4, true>(a, wfull, S, st);
+    } else {
+        if (RB >= 4)
+            return mfma_launch<KS, NSTS, 4, true>(a, wfull, S, st);
+        return mfma_launch<KS, NSTS, 4, false>(a, wfull, S, st);
+    }
 }
 
 static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
@@ -1794,8 +1820,10 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
             rc = mfma_dispatch<1>(a, wfull, S, st);
         else if (L.KS() == 2)
             rc = mfma_dispatch<2>(a, wfull, S, st);
-        else
+        else if (L.KS() == 4)
             rc = mfma_dispatch<4>(a, wfull, S, st);
+        else
+            rc = mfma_dispatch<8>(a, wfull, S, st);
         if (rc || wfull == words)
             return rc;
         a.ext.c0 = wfull;
@@ -1811,6 +1839,8 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
         return mat_dispatch<16>(cols, a, S, st);
     case 32:
         return mat_dispatch<32>(cols, a, S, st);
+    case 64:
+        return mat_dispatch<64>(cols, a, S, st);
     default:
         return -3;
     }
@@ -1848,10 +1878,17 @@ int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
                       long long ctx_stride, const Oor* in_oor, int slot_base,
                       int by_pos, long long words, uint32_t* err, hipStream_t st)
 {
-    if (k > 64 || S <= 0)
+    if (k > 128 || S <= 0)
         return -3;
     Oor none{nullptr, nullptr, 0, 0};
     const size_t lds = static_cast<size_t>(k) * ctx_pitch(k) * 4 * (mode ? 2 : 1);
+    // k > 64: up to 135 KB (systematic k = 128) of dynamic LDS, opted in
+    // per launch (cheap; the device may differ between calls)
+    if (lds > 65536 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_ctx_kernel<256>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(lds)) != hipSuccess)
+        return -2;
     if (k > 32)
         hipLaunchKernelGGL(decode_ctx_kernel<256>, dim3(S), dim3(256), lds, st, k, r,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,

@@ -15,18 +15,21 @@
 
 namespace qi {
 
-// Non-systematic encodes with K <= 64 run the register FNT codelets, except
-// at K = 64, where the matrix-core kernel over the Vandermonde generator is
-// faster (cfg3: 1.04 vs 1.17 ms, profiles/r2_ab_enc_matrix.txt): a 64-point
+// Non-systematic encodes with K <= 32 run the register FNT codelets; at
+// K = 64 the matrix-core kernel over the Vandermonde generator is faster
+// (cfg3: 1.04 vs 1.17 ms, profiles/r2_ab_enc_matrix.txt): a 64-point
 // codelet pass needs ~15.5 VALU per output, the MFMA epilogue ~6.  At
-// K = 16 (cfg2) the codelets win (3.65 vs 3.75 ms).  QI_ENC_MATRIX=1 / 0
-// forces either kernel (A/B and tests).
+// K = 16 (cfg2) the codelets win (3.65 vs 3.75 ms).  K = 128 has no codelet
+// (registers).  QI_ENC_MATRIX=1 / 0 forces either kernel at K <= 64 (A/B
+// and tests).
 static bool enc_matrix(int K)
 {
+    if (K > 64)
+        return true;
     const char* e = std::getenv("QI_ENC_MATRIX");
     if (e && (e[0] == '0' || e[0] == '1'))
         return e[0] == '1';
-    return K == 64;
+    return K >= 64;
 }
 
 static uint32_t addm(uint32_t a, uint32_t b)
@@ -160,12 +163,13 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
     (void)hipGetDevice(&p->device);
 
     bool ok = hipMalloc(&p->d_err, 4) == hipSuccess && hipMemset(p->d_err, 0, 4) == hipSuccess;
-    if (ok && p->K > 64) {
-        // k > 64: NTT-structured encode/decode (ntt.hip), any k + m <= 65536
+    if (ok && p->K > 128) {
+        // k > 128: NTT-structured encode/decode (ntt.hip), any k + m <= 65536
         p->ntt = 1;
         ok = ntt_plan_init(p) == 0;
     } else if (ok) {
-        // twist factors w^{v t} for the encode passes (K <= 64)
+        // twist factors w^{v t} for the encode passes (K <= 32; K = 64 and
+        // 128 encode on the matrix cores)
         if (!p->sys && !enc_matrix(p->K)) {
             const int passes = p->n / p->K;
             std::vector<int32_t> tw(static_cast<size_t>(passes) * p->K);

@@ -159,7 +159,7 @@ static void test_matrix(std::mt19937_64& g)
 
 static void test_matrix_mfma(std::mt19937_64& g)
 {
-    for (int kin : {1, 3, 16, 17, 33, 64}) {
+    for (int kin : {1, 3, 16, 17, 33, 64, 65, 100, 128}) {
         for (int R : {kin, 48}) {
             int KP = 2;
             while (KP < (kin + 1) / 2)

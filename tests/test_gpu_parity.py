@@ -222,10 +222,17 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
     (32, 32, 0, 2, 1024),
     (33, 31, 0, 2, 513),      # K = 64 codelet, k not a power of two
     (64, 960, 0, 2, 2048),    # cfg3 shape
-    # k > 64: the NTT-structured general path (ntt.hip)
-    (65, 63, 0, 2, 300),      # smallest general-path code
+    # 64 < k <= 128: matrix cores at KS = 8 (whole 1024-column tiles) and
+    # the dot2 kernel at KP = 64 (column tails)
+    (65, 63, 0, 2, 300),
+    (65, 63, 0, 2, 1024),
     (100, 28, 0, 2, 1000),
-    (100, 50, 1, 2, 999),     # systematic: interpolation + NTT_n encode
+    (100, 28, 0, 3, 2148),
+    (100, 50, 1, 2, 999),
+    (100, 50, 1, 2, 2048),    # systematic: generator + mode-1 contexts
+    (128, 128, 0, 2, 2048),
+    (128, 100, 1, 1, 1100),
+    # k > 128: the NTT-structured general path (ntt.hip)
     (200, 56, 0, 3, 1000),    # quadiron_fnt32_new(2, 200, 56, ...)
     (200, 56, 1, 2, 513),
     (256, 768, 0, 2, 700),    # n = 1024, len_2k = 512

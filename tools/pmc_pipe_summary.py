@@ -16,7 +16,7 @@ for f in ["p1", "p2", "p3"]:
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(p)):
-        name = r["Kernel_Name"].split("(")[0][:44]
+        name = r["Kernel_Name"].split("(")[0][:44] + " grid=" + r["Grid_Size"]
         agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[name].add(r["Dispatch_Id"])
     for name, dd in agg.items():
