@@ -1168,9 +1168,17 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             // without marks (cfg3 encode: wait_any 34 % of wave cycles).
             // (One loop body, no lambda: as a lambda the compiler indexed
             // y[] dynamically and moved it to scratch memory.)
+            // Only the marks inside this super tile's 64 columns are applied
+            // (a wave-uniform test on the LDS list: the list holds the route
+            // tile's marks, 1024 columns, so without it every super tile
+            // paid 80 VALU per mark of its whole route tile).
+            const uint32_t st0 = static_cast<uint32_t>(col0 + 64 * ST);
             for (int e = 0; e < n_lm; e++) {
-                const int pos = s_i[e];
-                const long long wc = s_col[e];
+                const uint32_t wcu = __builtin_amdgcn_readfirstlane(s_col[e]);
+                if (wcu - st0 >= 64u)
+                    continue;
+                const int pos = __builtin_amdgcn_readfirstlane(s_i[e]);
+                const long long wc = wcu;
                 const long long d = wc - cb;
                 const int32_t corr = plain[tcl * kin + pos];
 #pragma unroll
