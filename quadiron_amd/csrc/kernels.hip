@@ -1428,9 +1428,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
 {
     __shared__ uint32_t xs[128];
     __shared__ uint32_t A[129];
-    __shared__ uint32_t cinv[128];  // 1 / A'(x_i)
-    // k x k matrix (and the Q_i coefficients in systematic mode), sized by
-    // the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
+    __shared__ uint32_t cinv[128];    // 1 / A'(x_i)
+    __shared__ uint32_t aprime[128];  // A'(x_i)
+    // k x k matrix, sized by the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
     // limited the kernel to 4 workgroups per CU
     extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
     // row pitch = 4 x odd (>= k, a multiple of 4 words): the tile pass
@@ -1439,7 +1439,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // instruction at k = 64)
     const int kp = ctx_pitch(k);
     uint32_t* Mt = qi_ctx_lds;
-    uint32_t* Qt = qi_ctx_lds + k * kp;
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
     int32_t* mat = ctx + s * ctx_stride;
@@ -1521,23 +1520,43 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         // column scale 1 / A'(x_i) is applied by the packing pass.
         const uint32_t xi = xs[tid];
         uint32_t q = 1, h = 1;  // A[k]; Q_i(x_i) so far
-        uint32_t* dst = mode == 0 ? Mt : Qt;
-        dst[(k - 1) * kp + tid] = 1;
+        if (mode == 0)
+            Mt[(k - 1) * kp + tid] = 1;
         for (int j = k - 1; j >= 1; j--) {
             q = addm(A[j], mulm(xi, q));
-            dst[(j - 1) * kp + tid] = q;
+            if (mode == 0)
+                Mt[(j - 1) * kp + tid] = q;
             h = addm(mulm(h, xi), q);
         }
+        aprime[tid] = h;
         cinv[tid] = powm(h, 65535u);
-        if (mode != 0) {
-            // M[t][i] = Q_i(r^t) (/ A'(x_i) in the packing pass)
-            uint32_t e = 1;
-            for (int t = 0; t < k; t++) {
-                uint32_t acc = 0;
-                for (int j = k - 1; j >= 0; j--)
-                    acc = addm(mulm(acc, e), Qt[j * kp + tid]);
-                Mt[t * kp + tid] = acc;
-                e = mulm(e, r);
+    }
+    if (mode != 0) {
+        // systematic: M[t][i] = Q_i(r^t) / A'(x_i), one thread per row t,
+        // with Q_i(r^t) = A(r^t) / (r^t - x_i): 0 when r^t is another
+        // received point (A(r^t) = 0), A'(x_i) when it is x_i itself.  The
+        // k inverses of a row come from one inversion (prefix products, the
+        // running inverse walked back), so a row costs ~3k + 24 serial
+        // multiplies (Horner of every Q_i at every r^t took k^2 per lane).
+        __syncthreads();
+        if (tid < k) {
+            uint32_t* row = Mt + tid * kp;
+            const uint32_t et = powm(r, static_cast<uint32_t>(tid));
+            uint32_t av = 1;  // A(r^t), A monic
+            for (int j = k - 1; j >= 0; j--)
+                av = addm(mulm(av, et), A[j]);
+            uint32_t pre = 1;
+            for (int i = 0; i < k; i++) {
+                const uint32_t d = subm(et, xs[i]);
+                row[i] = pre;
+                pre = mulm(pre, d ? d : 1u);
+            }
+            uint32_t inv = powm(pre, 65535u);
+            for (int i = k - 1; i >= 0; i--) {
+                const uint32_t d = subm(et, xs[i]);
+                const uint32_t inv_i = mulm(inv, row[i]);
+                inv = mulm(inv, d ? d : 1u);
+                row[i] = d ? mulm(av, inv_i) : aprime[i];
             }
         }
     }
@@ -1889,8 +1908,8 @@ int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
     if (k > 128 || S <= 0)
         return -3;
     Oor none{nullptr, nullptr, 0, 0};
-    const size_t lds = static_cast<size_t>(k) * ctx_pitch(k) * 4 * (mode ? 2 : 1);
-    // k > 64: up to 135 KB (systematic k = 128) of dynamic LDS, opted in
+    const size_t lds = static_cast<size_t>(k) * ctx_pitch(k) * 4;
+    // k > 64: up to 68 KB (k = 128) of dynamic LDS, opted in
     // per launch (cheap; the device may differ between calls)
     if (lds > 65536 &&
         hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_ctx_kernel<256>),
