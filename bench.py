@@ -45,11 +45,12 @@ CONFIGS = {
     "cfg2": (16, 48, 65536, 4096),
     "cfg3": (64, 960, 4096, 1024),   # high fragmentation, n = 1024
     "cfg1": (4, 4, 1024, 100),       # the reference's CPU plumbing case
-    # larger codes: not BASELINE configs, extra lines.  64 < k <= 128 on
-    # the matrix cores, k > 128 on the NTT path
+    # larger codes: not BASELINE configs, extra lines.  64 < k <= 256 on
+    # the matrix cores, k > 256 on the NTT path
     "k128": (128, 128, 65536, 128),  # n = 256
-    "k200": (200, 56, 65536, 64),    # n = 256, len_2k = 512
-    "k256": (256, 768, 4096, 256),   # n = 1024, len_2k = 512
+    "k200": (200, 56, 65536, 64),    # n = 256
+    "k256": (256, 768, 4096, 256),   # n = 1024
+    "k300": (300, 212, 65536, 32),   # n = 512, len_2k = 1024 (NTT engine)
 }
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 

@@ -1156,8 +1156,9 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             for (int T = 0; T < 4; T++)
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    y[4 * T + j] = fold(fold((acc[T][2][j] << 8) + acc[T][1][j] -
-                                             acc[T][0][j]));
+                    y[4 * T + j] =
+                        fold(fold(((KS >= 16 ? fold(acc[T][2][j]) : acc[T][2][j]) << 8) +
+                                  acc[T][1][j] - acc[T][0][j]));
             // restored OOR symbols of the received rows: 65536 == -1 where
             // the stored word is 0 (decode_prepare, src/fec_base.h:1361-1404)
             // Branch-free per lane: the marks come from LDS and the
@@ -1302,7 +1303,7 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
 //   mode 1: M[t][i] = Q_i(r^t)   / A'(x_i)        (systematic)
 // plus the OOR route table of the stripe (decode_prepare's props walk,
 // src/fec_base.h:1361-1404, precomputed per tile).
-// One workgroup per stripe (64 lanes for k <= 32, else 256); k <= 128.
+// One workgroup per stripe (64 lanes for k <= 32, else 256); k <= 256.
 // ---------------------------------------------------------------------------
 // canonical a * b mod 65537 for a, b in [0, 65536]: with 2^16 = -1 and
 // 2^32 = 1, p = p0 + p1 2^16 + p2 2^32 reduces to p0 - p1 + p2
@@ -1420,16 +1421,16 @@ __host__ __device__ inline int ctx_pitch(int k)
     return (k + 3) / 8 * 8 + 4;
 }
 
-template <int NT>
+template <int NT, bool BIG>
 __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
     int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
     int by_pos, long long words, uint32_t* err)
 {
-    __shared__ uint32_t xs[128];
-    __shared__ uint32_t A[129];
-    __shared__ uint32_t cinv[128];    // 1 / A'(x_i)
-    __shared__ uint32_t aprime[128];  // A'(x_i)
+    __shared__ uint32_t xs[256];
+    __shared__ uint32_t A[257];
+    __shared__ uint32_t cinv[256];    // 1 / A'(x_i)
+    __shared__ uint32_t aprime[256];  // A'(x_i)
     // k x k matrix, sized by the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
     // limited the kernel to 4 workgroups per CU
     extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
@@ -1437,11 +1438,14 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // reads 16 rows x 16 bytes per wave (ds_read_b128) conflict-free (the
     // odd pitch k | 1 had SQ_LDS_BANK_CONFLICT at 7.4 cycles per LDS
     // instruction at k = 64)
-    const int kp = ctx_pitch(k);
-    uint32_t* Mt = qi_ctx_lds;
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
     int32_t* mat = ctx + s * ctx_stride;
+    // BIG (128 < k <= 256): the k x k matrix (up to 256 KB) does not fit
+    // LDS; its rows live in the context's own `plain` section (pitch k),
+    // which the packing pass rewrites in place with the row-scaled entries
+    const int kp = BIG ? k : ctx_pitch(k);
+    uint32_t* Mt = BIG ? reinterpret_cast<uint32_t*>(mat + L.plain()) : qi_ctx_lds;
     int32_t* cids = mat + L.words();
     uint32_t* route = reinterpret_cast<uint32_t*>(cids + 2 * L.KP);
     for (int i = k + tid; i < 2 * L.KP; i += NT)
@@ -1481,9 +1485,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             }
         }
     }
-    // A(x) = prod_i (x - x_i), lane d holding coefficient d (and d + 64
-    // for k > 64).  A is monic: A[k] = 1 is set explicitly, so k = 64 (128)
-    // needs no 65th (129th) coefficient slot.
+    // A(x) = prod_i (x - x_i), lane d holding coefficient d (and d + 64,
+    // d + 128, ... for k > 64).  A is monic: A[k] = 1 is set explicitly, so
+    // k = 64 (128, 256) needs no 65th (129th, 257th) coefficient slot.
     if (tid < 64) {  // wave 0 (wave-uniform)
         uint32_t a = tid == 0 ? 1u : 0u;
         if (k <= 64) {
@@ -1494,18 +1498,33 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                 a = subm(prev, mulm(xs[i], a));
             }
         } else {
-            uint32_t a1 = 0;
+            // slot u holds coefficient 64 u + lane (u < nslot <= 4)
+            const int nslot = (k + 63) / 64;
+            uint32_t au[4] = {a, 0u, 0u, 0u};
             for (int i = 0; i < k; i++) {
-                uint32_t prev = __shfl_up(a, 1), prev1 = __shfl_up(a1, 1);
-                const uint32_t top = __shfl(a, 63);  // coefficient 63 -> 64
-                if (tid == 0) {
-                    prev = 0;
-                    prev1 = top;
+                uint32_t prev[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    prev[u] = __shfl_up(au[u], 1);
+#pragma unroll
+                for (int u = 1; u < 4; u++) {
+                    const uint32_t top = __shfl(au[u - 1], 63);  // 64 u - 1 -> 64 u
+                    if (tid == 0)
+                        prev[u] = top;
                 }
-                a = subm(prev, mulm(xs[i], a));
-                a1 = subm(prev1, mulm(xs[i], a1));
+                if (tid == 0)
+                    prev[0] = 0;
+                const uint32_t x = xs[i];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (u < nslot)
+                        au[u] = subm(prev[u], mulm(x, au[u]));
             }
-            A[64 + tid] = a1;
+            a = au[0];
+#pragma unroll
+            for (int u = 1; u < 4; u++)
+                if (u < nslot)
+                    A[64 * u + tid] = au[u];
         }
         A[tid] = a;
         if (tid == 0)
@@ -1586,8 +1605,18 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             const int t = 16 * rb + tl4, i0 = 4 * j;
             uint32_t aw = 0, bw = 0;
             if (t < L.R && i0 < k) {
-                const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
-                const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
+                uint32_t e[4];
+                if constexpr (BIG) {  // global rows, pitch k: no 16-byte alignment
+#pragma unroll
+                    for (int jb = 0; jb < 4; jb++)
+                        e[jb] = i0 + jb < k ? Mt[t * kp + i0 + jb] : 0u;
+                } else {
+                    const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
+                    e[0] = e4.x;
+                    e[1] = e4.y;
+                    e[2] = e4.z;
+                    e[3] = e4.w;
+                }
 #pragma unroll
                 for (int jb = 0; jb < 4; jb++) {
                     if (i0 + jb < k) {
@@ -1731,7 +1760,9 @@ int matrix_kp(int kin)
         return 32;
     if (pairs <= 64)
         return 64;
-    return -1;  // k > 128 runs the NTT path (ntt.hip)
+    if (pairs <= 128)
+        return 128;
+    return -1;  // k > 256 runs the NTT path (ntt.hip)
 }
 
 template <int KP, int COLS, bool BUF>
@@ -1808,7 +1839,11 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
 {
     constexpr int NSTS = KS == 1 ? 16 : 8;
     const int RB = a.L.RB();
-    if constexpr (KS == 8) {
+    if constexpr (KS == 16) {
+        // 128 < k <= 256: a 512-row byte-plane image of 64 columns (41 KB)
+        (void)RB;
+        return mfma_launch<KS, 1, 4, true>(a, wfull, S, st);
+    } else if constexpr (KS == 8) {
         // 65 <= k <= 128: a 256-row byte-plane image, the waves always
         // splitting the row blocks (a wave past the last row block idles)
         // (256 columns, 81 KB with the staging tiles: 2 blocks per CU as
@@ -1850,8 +1885,10 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
             rc = mfma_dispatch<2>(a, wfull, S, st);
         else if (L.KS() == 4)
             rc = mfma_dispatch<4>(a, wfull, S, st);
-        else
+        else if (L.KS() == 8)
             rc = mfma_dispatch<8>(a, wfull, S, st);
+        else
+            rc = mfma_dispatch<16>(a, wfull, S, st);
         if (rc || wfull == words)
             return rc;
         a.ext.c0 = wfull;
@@ -1869,6 +1906,8 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
         return mat_dispatch<32>(cols, a, S, st);
     case 64:
         return mat_dispatch<64>(cols, a, S, st);
+    case 128:
+        return mat_dispatch<128>(cols, a, S, st);
     default:
         return -3;
     }
@@ -1906,23 +1945,29 @@ int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
                       long long ctx_stride, const Oor* in_oor, int slot_base,
                       int by_pos, long long words, uint32_t* err, hipStream_t st)
 {
-    if (k > 128 || S <= 0)
+    if (k > 256 || S <= 0)
         return -3;
     Oor none{nullptr, nullptr, 0, 0};
+    if (k > 128) {  // the matrix rows in the context itself (no LDS image)
+        hipLaunchKernelGGL((decode_ctx_kernel<256, true>), dim3(S), dim3(256), 0, st, k, r,
+                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
+                           slot_base, by_pos, words, err);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
     const size_t lds = static_cast<size_t>(k) * ctx_pitch(k) * 4;
     // k > 64: up to 68 KB (k = 128) of dynamic LDS, opted in
     // per launch (cheap; the device may differ between calls)
     if (lds > 65536 &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_ctx_kernel<256>),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_ctx_kernel<256, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds)) != hipSuccess)
         return -2;
     if (k > 32)
-        hipLaunchKernelGGL(decode_ctx_kernel<256>, dim3(S), dim3(256), lds, st, k, r,
+        hipLaunchKernelGGL((decode_ctx_kernel<256, false>), dim3(S), dim3(256), lds, st, k, r,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
                            slot_base, by_pos, words, err);
     else
-        hipLaunchKernelGGL(decode_ctx_kernel<64>, dim3(S), dim3(64), lds, st, k, r,
+        hipLaunchKernelGGL((decode_ctx_kernel<64, false>), dim3(S), dim3(64), lds, st, k, r,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
                            slot_base, by_pos, words, err);
     return hipGetLastError() == hipSuccess ? 0 : -2;

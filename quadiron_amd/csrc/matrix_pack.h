@@ -16,7 +16,7 @@ namespace qi {
 //   kcorr[R]       32768 * sum_i c[t][i] mod q (undoes the x - 32768 offset)
 //   rscale[R]      balanced inverse row scale (1 = unscaled)
 //   plain[R][kin]  canonical row-scaled entries (OOR corrections)
-//   mf[RB][KS][3][64][2]  i8 operand tiles of matrix_mfma_kernel (kin <= 128):
+//   mf[RB][KS][3][64][2]  i8 operand tiles of matrix_mfma_kernel (kin <= 256):
 //                  RB = ceil(R / 16) output blocks, KS = K-steps of 32
 //                  bytes, 3 operand types, 64 lanes x 8 bytes (pack_mf_dword)
 //   kmf[R]         32896 * sum_i c[t][i] mod q (undoes the byte offsets)
@@ -26,8 +26,8 @@ namespace qi {
 //                  that hit +-2^15 need no scale there (decode contexts use
 //                  one scale for both: rscale_mf = rscale)
 // The MFMA section exists (KS() > 0) when matrix_mfma_kernel takes the
-// block: kin <= 128 (|D2| <= 2 kin 128^2 = 2^22, so 256 D2 + D1 - D0 stays
-// inside int32).
+// block: kin <= 256.  |D2| <= 2 kin 128^2: up to k = 128 (2^22) 256 D2 +
+// D1 - D0 stays inside int32; at KS = 16 the epilogue folds D2 first.
 // A/B on MI355X, k = 16 decode: 1.54 ms on the matrix cores with the
 // LDS-transposed streaming stores vs 1.62 ms dot2 (1.65 ms before the
 // transpose); the 48 x 16 systematic encode 3.60 vs 3.80 ms and the 64 x 64
@@ -36,9 +36,9 @@ struct MatLayout {
     int R, kin, KP;
     QI_HD int KS() const
     {
-        if (kin > 128)
+        if (kin > 256)
             return 0;
-        return kin <= 16 ? 1 : kin <= 32 ? 2 : kin <= 64 ? 4 : 8;
+        return kin <= 16 ? 1 : kin <= 32 ? 2 : kin <= 64 ? 4 : kin <= 128 ? 8 : 16;
     }
     QI_HD int RB() const { return KS() ? (R + 15) / 16 : 0; }
     QI_HD size_t packed() const { return 0; }
@@ -149,8 +149,8 @@ QI_HD uint32_t pack_row(const uint32_t* row, const MatLayout& L, int t,
 // `plain` section, or a copy of it in LDS).
 QI_HD int32_t pack_mf_dword(const MatLayout& L, const int32_t* rows, size_t d)
 {
-    const int KS = L.KS(), KH = 16 * KS;  // KS is 1, 2, 4 or 8
-    const int sh = KS == 1 ? 0 : KS == 2 ? 1 : KS == 4 ? 2 : 3;
+    const int KS = L.KS(), KH = 16 * KS;  // KS is 1, 2, 4, 8 or 16
+    const int sh = KS == 1 ? 0 : KS == 2 ? 1 : KS == 4 ? 2 : KS == 8 ? 3 : 4;
     const int tile = static_cast<int>(d >> 7);
     const int rem = static_cast<int>(d & 127), lane = rem >> 1, dw = rem & 1;
     const int ty = tile % 3, rk = tile / 3;

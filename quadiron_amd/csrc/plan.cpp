@@ -19,8 +19,8 @@ namespace qi {
 // K = 64 the matrix-core kernel over the Vandermonde generator is faster
 // (cfg3: 1.04 vs 1.17 ms, profiles/r2_ab_enc_matrix.txt): a 64-point
 // codelet pass needs ~15.5 VALU per output, the MFMA epilogue ~6.  At
-// K = 16 (cfg2) the codelets win (3.65 vs 3.75 ms).  K = 128 has no codelet
-// (registers).  QI_ENC_MATRIX=1 / 0 forces either kernel at K <= 64 (A/B
+// K = 16 (cfg2) the codelets win (3.65 vs 3.75 ms).  K = 128, 256 have no
+// codelet (registers).  QI_ENC_MATRIX=1 / 0 forces either kernel at K <= 64 (A/B
 // and tests).
 static bool enc_matrix(int K)
 {
@@ -163,13 +163,13 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
     (void)hipGetDevice(&p->device);
 
     bool ok = hipMalloc(&p->d_err, 4) == hipSuccess && hipMemset(p->d_err, 0, 4) == hipSuccess;
-    if (ok && p->K > 128) {
-        // k > 128: NTT-structured encode/decode (ntt.hip), any k + m <= 65536
+    if (ok && p->K > 256) {
+        // k > 256: NTT-structured encode/decode (ntt.hip), any k + m <= 65536
         p->ntt = 1;
         ok = ntt_plan_init(p) == 0;
     } else if (ok) {
-        // twist factors w^{v t} for the encode passes (K <= 32; K = 64 and
-        // 128 encode on the matrix cores)
+        // twist factors w^{v t} for the encode passes (K <= 32; K = 64 to
+        // 256 encode on the matrix cores)
         if (!p->sys && !enc_matrix(p->K)) {
             const int passes = p->n / p->K;
             std::vector<int32_t> tw(static_cast<size_t>(passes) * p->K);

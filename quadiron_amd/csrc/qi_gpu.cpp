@@ -47,8 +47,8 @@ SlowList ctx_slow(const qi_plan* p, const void* d_ctx, long long words)
 }
 
 // Decode contexts for n_stripes stripes, built on the device inside the
-// caller's stream: k <= 128, interpolation matrices + OOR route tables
-// (decode_ctx_kernel); k > 128, the NTT decode's per-pattern constants
+// caller's stream: k <= 256, interpolation matrices + OOR route tables
+// (decode_ctx_kernel); k > 256, the NTT decode's per-pattern constants
 // (ntt_ctx_kernel; its decode reads the OOR buckets directly).
 int build_ctx(qi_plan* p, const uint16_t* d_ids, int n_stripes, const Oor* in,
               int slot_base, int by_pos, long long words, void* d_ctx, hipStream_t s)

@@ -159,7 +159,7 @@ static void test_matrix(std::mt19937_64& g)
 
 static void test_matrix_mfma(std::mt19937_64& g)
 {
-    for (int kin : {1, 3, 16, 17, 33, 64, 65, 100, 128}) {
+    for (int kin : {1, 3, 16, 17, 33, 64, 65, 100, 128, 129, 200, 256}) {
         for (int R : {kin, 48}) {
             int KP = 2;
             while (KP < (kin + 1) / 2)
@@ -211,7 +211,9 @@ static void test_matrix_mfma(std::mt19937_64& g)
                     }
                     for (long long d : D)
                         CHECK(d >= -2147483648LL && d <= 2147483647LL, "mfma acc overflow");
-                    const long long v = D[2] * 256 + D[1] - D[0];
+                    // KS = 16 (k > 128): the device folds D2 before the shift
+                    const long long d2 = KS >= 16 ? fold(static_cast<int32_t>(D[2])) : D[2];
+                    const long long v = d2 * 256 + D[1] - D[0];
                     CHECK(v >= -2147483648LL && v <= 2147483647LL, "mfma epilogue overflow");
                     int32_t y = fold(fold(static_cast<int32_t>(v)));
                     const int32_t rs = blk[L.rscale() + t];

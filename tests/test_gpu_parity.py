@@ -232,11 +232,19 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
     (100, 50, 1, 2, 2048),    # systematic: generator + mode-1 contexts
     (128, 128, 0, 2, 2048),
     (128, 100, 1, 1, 1100),
-    # k > 128: the NTT-structured general path (ntt.hip)
+    # 128 < k <= 256: matrix cores at KS = 16 (D2 folded in the epilogue),
+    # the context's matrix rows in global memory, dot2 tails at KP = 128
     (200, 56, 0, 3, 1000),    # quadiron_fnt32_new(2, 200, 56, ...)
+    (200, 56, 0, 2, 2112),
     (200, 56, 1, 2, 513),
-    (256, 768, 0, 2, 700),    # n = 1024, len_2k = 512
-    (130, 900, 1, 1, 300),    # systematic, n = 2048 > len_2k
+    (200, 56, 1, 2, 1024),
+    (256, 768, 0, 2, 700),
+    (256, 768, 0, 1, 2048),
+    (129, 127, 1, 1, 1100),
+    (130, 900, 1, 1, 300),
+    # k > 256: the NTT-structured general path (ntt.hip)
+    (257, 255, 0, 1, 300),    # smallest NTT-path code
+    (300, 100, 1, 1, 300),    # systematic: interpolation + NTT_n encode
     (1000, 24, 0, 1, 260),    # len_2k = 2048 > n = 1024
 ])
 def test_batch_vs_oracle(k, m, sys_, S, P):
@@ -260,10 +268,11 @@ def _eval_rows(data, rows, n, sys_):
 
 
 @pytest.mark.parametrize("k,m,sys_,S,P", [
-    (130, 16000, 0, 1, 4500),   # n = 16384: the columns run in 2 slices
-    (100, 3000, 0, 70, 256),    # n = 4096, 70 stripes: 2 stripe groups
-    (200, 56, 0, 600, 256),     # LDS engine over 600 stripes x 8 tiles
-    (100, 16000, 1, 1, 4200),   # systematic, sliced
+    (300, 16000, 0, 1, 4500),   # n = 16384: the columns run in 2 slices
+    (300, 3000, 0, 70, 256),    # n = 4096, 70 stripes: 2 stripe groups
+    (260, 200, 0, 600, 256),    # LDS engine over 600 stripes x 8 tiles
+    (260, 16000, 1, 1, 4200),   # systematic, sliced
+    (130, 16000, 0, 1, 4500),   # matrix path: a 16130 x 130 generator
 ])
 def test_general_path_slicing(k, m, sys_, S, P):
     """The general path's multi-pass engine (max(n, len_2k) > 2048) cuts a

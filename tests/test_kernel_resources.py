@@ -15,7 +15,7 @@ RES = [os.path.join(ROOT, "build", "obj", f) for f in ("kernels.res", "ntt.res")
 # K = 64 encode codelet (256 VGPRs at 2 waves/SIMD, 3-4 spilled registers;
 # 3 waves/SIMD spilled 280 and ran 20 % slower, profiles/r1_ab_k64_encode.txt)
 ALLOWED = ("matrix_redo_kernel", "encode_fnt_kernelILi64E",
-           "matrix_kernelILi64E")  # the dot2 column tails at 64 < k <= 128
+           "matrix_kernelILi64E", "matrix_kernelILi128E")  # dot2 column tails, k > 64
 
 
 def kernels():
@@ -53,7 +53,7 @@ def test_mfma_kernel_occupancy():
     LDS images allow 4 blocks of 4 waves per CU at k <= 16); the k <= 128
     kernel (KS = 8, 200 VGPRs) keeps 2."""
     for k, v in kernels().items():
-        if "matrix_mfma_kernelILi8E" in k:
+        if "matrix_mfma_kernelILi8E" in k or "matrix_mfma_kernelILi16E" in k:
             assert v.get("Occupancy", 0) >= 2, (k, v)
         elif "matrix_mfma_kernel" in k:
             assert v.get("Occupancy", 0) >= 4, (k, v)
