@@ -1364,12 +1364,26 @@ __device__ __forceinline__ uint32_t grp_add(uint32_t v, int lpr)
 __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLayout& L,
                              int t, int32_t* block, int sub, int lpr)
 {
+    // the lane's entries i = sub + m lpr (m < 16: k <= 256 at lpr = 16) in
+    // registers: every row load is issued up front (rows in global memory
+    // for k > 128), and the packed pairs take the odd entry from the
+    // neighbour lane by shuffle instead of re-reading the row
+    constexpr int ME = 16;
     const int kin = L.kin, KP = L.KP;
+    uint32_t v[ME];
+#pragma unroll
+    for (int m = 0; m < ME; m++) {
+        const int i = sub + m * lpr;
+        v[m] = i < kin ? row[i] : 0u;
+    }
     uint32_t bad = 0;
-    for (int i = sub; i < kin; i += lpr) {
-        const uint32_t c = mulm(row[i], cscale[i]);
-        row[i] = c;
-        bad |= !coef_ok(balanced(c));
+#pragma unroll
+    for (int m = 0; m < ME; m++) {
+        const int i = sub + m * lpr;
+        if (i < kin) {
+            v[m] = mulm(v[m], cscale[i]);
+            bad |= !coef_ok(balanced(v[m]));
+        }
     }
     bad = grp_or(bad, lpr);
     uint32_t s = 1;
@@ -1379,33 +1393,45 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
         if (iabs32(si) > 32766)
             continue;
         bad = 0;
-        for (int i = sub; i < kin; i += lpr)
-            bad |= !coef_ok(balanced(mulm(row[i], s)));
+#pragma unroll
+        for (int m = 0; m < ME; m++) {
+            const int i = sub + m * lpr;
+            if (i < kin)
+                bad |= !coef_ok(balanced(mulm(v[m], s)));
+        }
         bad = grp_or(bad, lpr);
-    }
-    if (s != 1) {  // every lane of the group reads only its own entries
-        for (int i = sub; i < kin; i += lpr)
-            row[i] = mulm(row[i], s);
     }
     int32_t* packed = block + static_cast<size_t>(t) * KP;
     int32_t* plain = block + L.plain();
-    for (int j = sub; j < KP; j += lpr) {
-        const int32_t lo = 2 * j < kin ? balanced(row[2 * j]) : 0;
-        const int32_t hi = 2 * j + 1 < kin ? balanced(row[2 * j + 1]) : 0;
-        packed[j] = static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xffffu) |
-                                         (static_cast<uint32_t>(hi) << 16));
+    uint32_t sum = 0;  // <= 256 * 65536 = 2^24
+#pragma unroll
+    for (int m = 0; m < ME; m++) {
+        const int i = sub + m * lpr;
+        if (s != 1 && i < kin)
+            v[m] = mulm(v[m], s);
+        // pair (i, i + 1) for even i: the odd entry sits on lane sub + 1
+        const uint32_t odd = __shfl_xor(v[m], 1, lpr);
+        if (i < kin) {
+            row[i] = v[m];
+            plain[static_cast<size_t>(t) * kin + i] = static_cast<int32_t>(v[m]);
+            sum += v[m];
+            if (!(sub & 1)) {
+                const int32_t lo = balanced(v[m]);
+                const int32_t hi = i + 1 < kin ? balanced(odd) : 0;
+                packed[i >> 1] = static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xffffu) |
+                                                      (static_cast<uint32_t>(hi) << 16));
+            }
+        }
     }
-    uint32_t sum = 0;  // <= 64 * 65536 < 2^23
-    for (int i = sub; i < kin; i += lpr) {
-        const uint32_t c = row[i];
-        plain[static_cast<size_t>(t) * kin + i] = static_cast<int32_t>(c);
-        sum += c;
-    }
+    // pairs past kin up to KP stay zero (the dot2 kernel's padding)
+    for (int j = (kin + 1) / 2 + sub; j < KP; j += lpr)
+        packed[j] = 0;
     sum = grp_add(sum, lpr);
     if (sub == 0) {
-        // sum mod q by one fold (2^16 = -1): [-127, 65535] -> canonical
-        const int32_t f = static_cast<int32_t>(sum & 0xffffu) - static_cast<int32_t>(sum >> 16);
-        const uint32_t sq = static_cast<uint32_t>(f < 0 ? f + 65537 : f);
+        // sum mod q by two folds (2^16 = -1), then canonical
+        int32_t f = static_cast<int32_t>(sum & 0xffffu) - static_cast<int32_t>(sum >> 16);
+        f = f < 0 ? f + 65537 : f;
+        const uint32_t sq = static_cast<uint32_t>(f >= 65537 ? f - 65537 : f);
         block[L.kcorr() + t] = static_cast<int32_t>(mulm(sq, 32768u));
         block[L.rscale() + t] = s == 1 ? 1 : balanced(powm(s, 65535u));
         if (L.KS()) {
@@ -1599,45 +1625,64 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         // matrix_mfma_kernel skips those K-steps (and never loads them).
         const int KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
         int32_t* mf = mat + L.mf();
-        for (int it = tid; it < RB * nj * 16; it += NT) {
-            const int tl4 = it & 15, jj = it >> 4;
-            const int j = jj % nj, rb = jj / nj;
-            const int t = 16 * rb + tl4, i0 = 4 * j;
-            uint32_t aw = 0, bw = 0;
-            if (t < L.R && i0 < k) {
-                uint32_t e[4];
+        // BIG: the rows come from global memory; 4 items per thread have
+        // their loads in flight together (the stores to the tiles may alias
+        // the rows as far as the compiler knows, so it would not overlap
+        // the iterations itself)
+        constexpr int IB = BIG ? 4 : 1;
+        const int items = RB * nj * 16;
+        for (int it0 = tid; it0 < items; it0 += IB * NT) {
+            uint32_t e[IB][4];
+#pragma unroll
+            for (int ib = 0; ib < IB; ib++) {
+                const int it = it0 + ib * NT;
+                const int tl4 = it & 15, jj = it >> 4;
+                const int t = 16 * (jj / nj) + tl4, i0 = 4 * (jj % nj);
+                const bool live = it < items && t < L.R && i0 < k;
                 if constexpr (BIG) {  // global rows, pitch k: no 16-byte alignment
 #pragma unroll
                     for (int jb = 0; jb < 4; jb++)
-                        e[jb] = i0 + jb < k ? Mt[t * kp + i0 + jb] : 0u;
-                } else {
+                        e[ib][jb] = live && i0 + jb < k ? Mt[t * kp + i0 + jb] : 0u;
+                } else if (live) {
                     const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
-                    e[0] = e4.x;
-                    e[1] = e4.y;
-                    e[2] = e4.z;
-                    e[3] = e4.w;
-                }
-#pragma unroll
-                for (int jb = 0; jb < 4; jb++) {
-                    if (i0 + jb < k) {
-                        int32_t a, b;
-                        split_i8(e[jb], a, b);
-                        aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
-                        bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
-                    }
+                    e[ib][0] = e4.x;
+                    e[ib][1] = e4.y;
+                    e[ib][2] = e4.z;
+                    e[ib][3] = e4.w;
                 }
             }
 #pragma unroll
-            for (int half = 0; half < 2; half++) {
-                const int K = half * KH + i0;
-                const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
-                const size_t base =
-                    static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl4) * 2 + dw;
-                if (KS < 4 || half == 0)
-                    mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
-                if (KS < 4 || half == 1)
-                    mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
-                mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
+            for (int ib = 0; ib < IB; ib++) {
+                const int it = it0 + ib * NT;
+                if (it >= items)
+                    break;
+                const int tl4 = it & 15, jj = it >> 4;
+                const int j = jj % nj, rb = jj / nj;
+                const int t = 16 * rb + tl4, i0 = 4 * j;
+                uint32_t aw = 0, bw = 0;
+                if (t < L.R && i0 < k) {
+#pragma unroll
+                    for (int jb = 0; jb < 4; jb++) {
+                        if (i0 + jb < k) {
+                            int32_t a, b;
+                            split_i8(e[ib][jb], a, b);
+                            aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
+                            bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int half = 0; half < 2; half++) {
+                    const int K = half * KH + i0;
+                    const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
+                    const size_t base =
+                        static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl4) * 2 + dw;
+                    if (KS < 4 || half == 0)
+                        mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
+                    if (KS < 4 || half == 1)
+                        mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
+                    mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
+                }
             }
         }
     }
@@ -1840,7 +1885,9 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
     constexpr int NSTS = KS == 1 ? 16 : 8;
     const int RB = a.L.RB();
     if constexpr (KS == 16) {
-        // 128 < k <= 256: a 512-row byte-plane image of 64 columns (41 KB)
+        // 128 < k <= 256: a 512-row byte-plane image of 64 columns (41 KB);
+        // 8 waves over 128 columns (94 KB, 1 block per CU) measured the
+        // same at k200 / k256 (profiles/r2_ab_round2b.txt)
         (void)RB;
         return mfma_launch<KS, 1, 4, true>(a, wfull, S, st);
     } else if constexpr (KS == 8) {
