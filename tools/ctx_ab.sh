@@ -1,6 +1,12 @@
-set -o pipefail
-mkdir -p gpurun_out/ctx
-for v in main g4; do
-  L=quadiron_amd/libquadiron_amd.so; [ $v != main ] && L=build/ab/$v/libquadiron_amd.so
-  QI_LIB_PATH=$L timeout -k 10 120 python3 tools/ctx_time.py > gpurun_out/ctx/$v.log 2>&1 || exit $?
+#!/bin/bash
+# decode-context timing: product vs build/ab/<variant>, alternating twice
+#   bash tools/ctx_ab.sh <tag> <variant>...
+T=$1; shift
+O=gpurun_out/$T
+mkdir -p $O
+for i in 1 2; do
+  timeout -k 10 120 python3 tools/ctx_time.py > $O/ctx_main_$i.log 2>&1 || exit $?
+  for v in "$@"; do
+    QI_LIB_PATH=build/ab/$v/libquadiron_amd.so timeout -k 10 120 python3 tools/ctx_time.py > $O/ctx_${v}_$i.log 2>&1 || exit $?
+  done
 done

@@ -15,7 +15,10 @@ timeout -k 10 300 python3 bench.py --cfg cfg1 > $O/bench_cfg1.log 2>&1 &&
 timeout -k 10 300 python3 bench.py --cfg k128 --steps 10 > $O/bench_k128.log 2>&1 &&
 timeout -k 10 300 python3 bench.py --cfg k200 --steps 5 > $O/bench_k200.log 2>&1 &&
 timeout -k 10 300 python3 bench.py --cfg k256 --steps 5 > $O/bench_k256.log 2>&1 &&
+timeout -k 10 300 python3 bench.py --cfg k300 --steps 3 > $O/bench_k300.log 2>&1 &&
 bash tools/prof.sh $O/prof --steps 10 --no-cpu-baseline &&
 bash tools/prof.sh $O/prof_cfg3 --cfg cfg3 --steps 10 --no-cpu-baseline &&
 bash tools/prof.sh $O/prof_k128 --cfg k128 --steps 5 --no-cpu-baseline &&
+bash tools/prof.sh $O/prof_k200 --cfg k200 --steps 5 --no-cpu-baseline &&
+bash tools/prof.sh $O/prof_k256 --cfg k256 --steps 5 --no-cpu-baseline &&
 bash tools/pmc.sh $O/pmc --steps 3 --warmup 1
