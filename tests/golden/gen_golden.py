@@ -227,6 +227,9 @@ def main():
     gen_blocks(ref, ora, "blk_k100_m28", 100, 28, 0, 64, 1200 + 6, 34, 3, 8, out)
     gen_cabi(ref, ora, "cabi_k200_m56", 200, 56, 0, 1500 + 2, 35, 2, 8, out)
     gen_cabi(ref, ora, "cabi_k130_m30_sys", 130, 30, 1, 2000, 36, 2, 8, out)
+    # k > 256: the NTT-structured path (k <= 256 moved to the matrix cores)
+    gen_blocks(ref, ora, "blk_k300_m212", 300, 212, 0, 128, 600 + 2, 37, 2, 8, out)
+    gen_blocks(ref, ora, "blk_k260_m30_sys", 260, 30, 1, 256, 512, 38, 2, 8, out)
 
 
 if __name__ == "__main__":
