@@ -44,8 +44,9 @@ int qi_gpu_device_count(void);
 
 /* Create an RS-FNT plan (word_size 2 only).  Returns NULL on bad
  * parameters (k < 1, m < 1, k+m > 65536) or when no device is present.
- * k <= 64 runs the register-codelet / matrix-core kernels, k > 64 the
- * NTT-structured general path (column-batched NTT passes). */
+ * k <= 256 runs the register-codelet (non-systematic k <= 32) and
+ * matrix-core kernels, k > 256 the NTT-structured general path
+ * (column-batched NTT passes). */
 qi_plan* qi_plan_create(int k, int m, int systematic);
 void qi_plan_destroy(qi_plan* plan);
 /* n (FFT length) and n_outputs (m if systematic, k+m otherwise) */
@@ -76,8 +77,9 @@ size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
  * src/fec_base.h:1199-1236) -- and route the OOR marks of those fragments
  * (buckets as produced by qi_gpu_encode; NULL counts = none) into per-tile
  * tables.  Built on the device, asynchronously on `stream`, for every k
- * (k > 64: the NTT decode's per-pattern constants, src/fec_context.h:232-274;
- * its decode reads the OOR buckets directly).  h_ids is unused (kept for
+ * (k <= 256: the interpolation matrix, up to ~780 KB per stripe at k = 256;
+ * k > 256: the NTT decode's per-pattern constants, src/fec_context.h:232-274,
+ * whose decode reads the OOR buckets directly).  h_ids is unused (kept for
  * ABI stability; may be NULL). */
 int qi_gpu_decode_ctx(qi_plan* plan, const uint16_t* d_ids,
                       const uint16_t* h_ids, int n_stripes,
