@@ -454,126 +454,115 @@ struct OorScan {
 // the decode context); matrix_redo_kernel, launched right after them on the
 // same stream, recomputes every column of the tile that holds a mark from
 // scratch -- all marks of the column restored, plain canonical arithmetic
-// -- and stores it again.  A column with several marks is recomputed by
-// several threads, which write the same words.  Only decodes carry input
-// marks, and their outputs are data symbols (< 65536), so nothing is
-// recorded as OOR here.  Keeping this out of the hot kernels keeps their
-// registers: inlined at their end it held the bucket and row pointers live
-// across the MFMA loop (SGPR spills, 2x slower decode).
+// -- and stores it again.  Only decodes carry input marks, and their
+// outputs are data symbols (< 65536), so nothing is recorded as OOR here.
+// Keeping this out of the hot kernels keeps their registers: inlined at
+// their end it held the bucket and row pointers live across the MFMA loop
+// (SGPR spills, 2x slower decode).
 __device__ __forceinline__ void push_slow_tile(const SlowList& sl, int s, long long col0,
                                                int width)
 {
+    // width: a power-of-two multiple of kSlowGrain (64 .. 1024 columns)
     uint32_t* l = sl.base + s * sl.stride;
     const uint32_t idx = atomicAdd(l, 1u);
-    l[1 + idx] = static_cast<uint32_t>(col0 / 256) << 2 |
-                 static_cast<uint32_t>(ilog2c(static_cast<uint32_t>(width / 256)));
+    l[1 + idx] = static_cast<uint32_t>(col0 / kSlowGrain) << 3 |
+                 static_cast<uint32_t>(ilog2c(static_cast<uint32_t>(width / kSlowGrain)));
 }
 
-__device__ void redo_marked_columns(const MatLayout& L, const int32_t* M,
-                                                 const RowSrc& src, const RowDst& dst,
-                                                 const OorScan& sc, long long col0,
-                                                 long long col1, const int32_t* rowmap)
-{
-    const int kin = L.kin;
-    const int32_t* rscale = M + L.rscale();
-    const int32_t* plain = M + L.plain();
-    auto row_of = [&](int i) -> const uint16_t* {
-        const int id = src.by_pos ? i : (sc.sid ? sc.sid[i] : i);
-        return id < src.split ? src.base0 + sc.s * src.ss0 + id * src.rs0
-                              : src.base1 + sc.s * src.ss1 + (id - src.split) * src.rs1;
-    };
-    auto slot_of = [&](int i) {
-        const int id = sc.sid ? sc.sid[i] : i;
-        return (sc.by_pos ? i : id) - sc.slot_base;
-    };
-    // walk every mark (i, e) of the tile, one per thread
-    int base = 0;
-    for (int i = 0; i < kin; i++) {
-        const int slot = slot_of(i);
-        if (slot < 0)
-            continue;
-        const long long bk = static_cast<long long>(sc.s) * sc.in.slots + slot;
-        const int cnt = static_cast<int>(min(sc.in.counts[bk],
-                                             static_cast<uint32_t>(sc.in.cap)));
-        for (int e = static_cast<int>(threadIdx.x) - base; e < cnt;
-             e += static_cast<int>(blockDim.x)) {
-            if (e < 0)
-                continue;
-            const long long w = sc.in.entries[bk * sc.in.cap + e];
-            if (w < col0 || w >= col1)
-                continue;
-            for (int t = 0; t < L.R; t++) {
-                uint64_t acc = 0;
-                for (int j = 0; j < kin; j++) {
-                    uint32_t x = row_of(j)[w];
-                    const int sj = slot_of(j);
-                    if (sj >= 0) {  // restored 65536 at every mark of column w
-                        const long long bj = static_cast<long long>(sc.s) * sc.in.slots + sj;
-                        const uint32_t cj = min(sc.in.counts[bj],
-                                                static_cast<uint32_t>(sc.in.cap));
-                        for (uint32_t f = 0; f < cj; f++)
-                            if (sc.in.entries[bj * sc.in.cap + f] == w)
-                                x = 65536u;
-                    }
-                    acc += static_cast<uint64_t>(static_cast<uint32_t>(plain[t * kin + j])) * x;
-                }
-                uint32_t y = static_cast<uint32_t>(acc % 65537u);
-                const int32_t rs = rscale[t];
-                if (rs != 1)
-                    y = static_cast<uint32_t>(
-                        static_cast<uint64_t>(y) * static_cast<uint32_t>(rs < 0 ? rs + kQ : rs) %
-                        65537u);
-                dst.base[sc.s * dst.ss + rowmap[t] * dst.rs + w] =
-                    static_cast<uint16_t>(y == 65536u ? 0u : y);
-            }
-        }
-        base = (base + cnt) % static_cast<int>(blockDim.x);
-    }
-}
+// One block per stripe at a time; a slow tile is redone in chunks of
+// kRedoCols columns: the chunk's received symbols (u16) and a bitmap of
+// their marks staged in LDS (every mark of every received row, from the
+// buckets), then lane c of wave wv recomputes column c for the output rows
+// wv, wv + 4, ... (the coefficient plain[t][j] is wave-uniform: scalar
+// loads) -- only in columns that hold a mark.  Work per chunk is
+// R * kin * 64 multiply-adds whatever the mark density (walking the marks
+// per (mark, row, input) was quadratic in the density).  The stripe's list
+// is emptied afterwards (a context can serve several decodes).
+constexpr int kRedoCols = 64;
 
-// see push_slow_tile: one block per stripe at a time; the stripe's list is
-// emptied afterwards (a context can serve several decodes)
 __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_stripes)
 {
+    __shared__ uint16_t xs[256 * kRedoCols];  // [input i][column]
+    __shared__ uint32_t mk[256 * (kRedoCols / 32)];
+    __shared__ uint32_t colmk[kRedoCols / 32];
     const MatLayout L = a.L;
-    const int32_t* __restrict__ mat = a.mat;
-    const long long mat_stride = a.ms;
-    const int32_t* __restrict__ ids = a.ids;
-    const long long ids_stride = a.is;
+    const int kin = L.kin;
     const RowSrc src = a.src;
     const RowDst dst = a.dst;
-    const MatExt ext = a.ext;
-    const long long words = a.words;
-    const int tiles = a.tiles;
-    const Oor in_oor = a.in_oor;
-    const int slot_base = a.slot_base;
-    const Oor out_oor = a.out_oor;
-    const uint32_t* __restrict__ route = a.route;
-    const long long route_stride = a.rstride;
-    const SlowList slow = a.slow;
-    uint32_t* err = a.err;
-    (void)ext;
-    (void)tiles;
-    (void)out_oor;
-    (void)route;
-    (void)route_stride;
-    (void)err;
+    const Oor in = a.in_oor;
+    const int tid = threadIdx.x, c = tid & 63, wv = tid >> 6;
     for (int s = blockIdx.x; s < n_stripes; s += gridDim.x) {
-        uint32_t* l = slow.base + s * slow.stride;
+        uint32_t* l = a.slow.base + s * a.slow.stride;
         const uint32_t n = __hip_atomic_load(l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (n == 0)
             continue;  // block-uniform
-        const OorScan sc{in_oor, ids ? ids + s * ids_stride : nullptr, src.by_pos,
-                         slot_base, L.kin, s, true};
-        for (uint32_t i = 0; i < n; i++) {
-            const uint32_t code = l[1 + i];
-            const long long col0 = static_cast<long long>(code >> 2) * 256;
-            const long long col1 = col0 + (256LL << (code & 3));
-            redo_marked_columns(L, mat + s * mat_stride, src, dst, sc, col0,
-                                col1 < words ? col1 : words, a.rowmap);
+        const int32_t* M = a.mat + s * a.ms;
+        const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
+        const int32_t* rscale = M + L.rscale();
+        const int32_t* plain = M + L.plain();
+        auto id_of = [&](int i) { return src.by_pos ? i : (sid ? sid[i] : i); };
+        for (uint32_t e = 0; e < n; e++) {
+            const uint32_t code = l[1 + e];
+            const long long t0 = static_cast<long long>(code >> 3) * kSlowGrain;
+            const long long t1 = min(t0 + (static_cast<long long>(kSlowGrain) << (code & 7)),
+                                     a.words);
+            for (long long c0 = t0; c0 < t1; c0 += kRedoCols) {
+                for (int j = tid; j < kin * (kRedoCols / 32); j += kBlock)
+                    mk[j] = 0;
+                if (tid < kRedoCols / 32)
+                    colmk[tid] = 0;
+                // the chunk's received symbols, one row of 64 per wave pass
+                for (int i = wv; i < kin; i += kBlock / 64) {
+                    const int id = id_of(i);
+                    const uint16_t* row =
+                        id < src.split ? src.base0 + s * src.ss0 + id * src.rs0
+                                       : src.base1 + s * src.ss1 + (id - src.split) * src.rs1;
+                    xs[i * kRedoCols + c] = c0 + c < t1 ? row[c0 + c] : 0;
+                }
+                __syncthreads();
+                // every mark of every received row inside the chunk
+                for (int i = tid; i < kin; i += kBlock) {
+                    const int slot = (src.by_pos ? i : id_of(i)) - a.slot_base;
+                    if (slot < 0)
+                        continue;  // systematic data row: no marks
+                    const long long bk = static_cast<long long>(s) * in.slots + slot;
+                    const uint32_t cnt = min(in.counts[bk], static_cast<uint32_t>(in.cap));
+                    for (uint32_t f = 0; f < cnt; f++) {
+                        const long long w = in.entries[bk * in.cap + f];
+                        if (w >= c0 && w < c0 + kRedoCols && w < t1) {
+                            const int cc = static_cast<int>(w - c0);
+                            atomicOr(&mk[i * (kRedoCols / 32) + cc / 32], 1u << (cc % 32));
+                            atomicOr(&colmk[cc / 32], 1u << (cc % 32));
+                        }
+                    }
+                }
+                __syncthreads();
+                if ((colmk[c / 32] >> (c % 32)) & 1u) {
+                    for (int t = wv; t < L.R; t += kBlock / 64) {
+                        uint64_t acc = 0;
+                        for (int j = 0; j < kin; j++) {
+                            const uint32_t x =
+                                (mk[j * (kRedoCols / 32) + c / 32] >> (c % 32)) & 1u
+                                    ? 65536u
+                                    : xs[j * kRedoCols + c];
+                            acc += static_cast<uint64_t>(
+                                       static_cast<uint32_t>(plain[t * kin + j])) * x;
+                        }
+                        uint32_t y = static_cast<uint32_t>(acc % 65537u);
+                        const int32_t rs = rscale[t];
+                        if (rs != 1)
+                            y = static_cast<uint32_t>(
+                                static_cast<uint64_t>(y) *
+                                static_cast<uint32_t>(rs < 0 ? rs + kQ : rs) % 65537u);
+                        dst.base[s * dst.ss + a.rowmap[t] * dst.rs + c0 + c] =
+                            static_cast<uint16_t>(y == 65536u ? 0u : y);
+                    }
+                }
+                __syncthreads();
+            }
         }
         __syncthreads();
-        if (threadIdx.x == 0)
+        if (tid == 0)
             *l = 0;
     }
 }

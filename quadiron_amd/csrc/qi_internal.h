@@ -62,17 +62,22 @@ struct Oor {
 // Per-stripe list of the column tiles whose received-row OOR marks overflowed
 // the matrix kernels' LDS list (more than 256 in one tile; adversarial
 // data).  Kept in the decode context: word 0 = count, then one word per
-// tile (col0 / 256) << 2 | log2(width / 256).  Capacity slow_words(words) - 1
-// covers every tile of a stripe.  launch_matrix runs matrix_redo_kernel
-// over it right after the matrix kernels.
+// tile (col0 / 64) << 3 | log2(width / 64).  Every kernel tile is a
+// power-of-two multiple of kSlowGrain = 64 columns (the narrowest, KS = 16
+// matrix-core blocks) starting on a multiple of its width, and each tile is
+// pushed at most once per launch, so capacity slow_words(words) - 1 =
+// ceil(words / 64) covers every tile of a stripe.  launch_matrix runs
+// matrix_redo_kernel over it right after the matrix kernels.
 struct SlowList {
     uint32_t* base;  // stripe s at base + s * stride (nullptr: no input marks)
     long long stride;
 };
 
+constexpr int kSlowGrain = 64;
+
 __host__ __device__ inline long long slow_words(long long words)
 {
-    return 1 + (words + 255) / 256;
+    return 1 + (words + kSlowGrain - 1) / kSlowGrain;
 }
 
 // ---- launchers (kernels.hip) ----

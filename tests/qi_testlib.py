@@ -163,6 +163,56 @@ def craft_oor_columns(k, m, sys_, data_rows, rng, n_cols, rows=None, col_range=N
             data_rows[0, j] = d0
 
 
+def _solve_mod(A, b):
+    """x with A x = b (mod Q) by Gaussian elimination, or None if singular."""
+    n = len(A)
+    M = [list(A[i]) + [b[i]] for i in range(n)]
+    for c in range(n):
+        piv = next((r for r in range(c, n) if M[r][c] % Q), None)
+        if piv is None:
+            return None
+        M[c], M[piv] = M[piv], M[c]
+        inv = pow(M[c][c], Q - 2, Q)
+        M[c] = [v * inv % Q for v in M[c]]
+        for r in range(n):
+            if r != c and M[r][c]:
+                f = M[r][c]
+                M[r] = [(vr - f * vc) % Q for vr, vc in zip(M[r], M[c])]
+    return [M[i][n] for i in range(n)]
+
+
+def craft_dense_oor(k, m, data_rows, rng, cols, rows, per_col):
+    """Non-systematic: make `per_col` distinct outputs among `rows` equal
+    65536 (OOR) in every column of `cols`, by solving for data rows
+    0..per_col-1 of that column.  Returns the number of columns crafted."""
+    o = oracle()
+    c = codec(k, m, 0)
+    cw = (C.c_uint32 * c.n)()
+    din = (C.c_uint32 * k)()
+
+    def enc(vals):
+        for t in range(k):
+            din[t] = int(vals[t])
+        o.qo_encode_column(C.byref(c), None, din, cw)
+        return [cw[i] for i in range(c.n_outputs)]
+
+    G = [enc([1 if t == u else 0 for t in range(k)]) for u in range(per_col)]
+    rows = list(rows)
+    done = 0
+    for j in cols:
+        col = data_rows[:, j].astype(np.int64)
+        col[:per_col] = 0
+        b = enc(col)
+        sel = rng.choice(rows, per_col, replace=False)
+        A = [[G[u][int(i)] for u in range(per_col)] for i in sel]
+        x = _solve_mod(A, [(65536 - b[int(i)]) % Q for i in sel])
+        if x is None or any(v == 65536 for v in x):
+            continue
+        data_rows[:per_col, j] = x
+        done += 1
+    return done
+
+
 def chunk_windows(words, chunk=1 << 21, width=4096):
     """Column windows [lo, hi) around the start, every stream-chunk boundary
     and the tail of a `words`-column block."""

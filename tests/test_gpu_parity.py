@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from qi_testlib import (Q, check_windows_vs_oracle, chunk_windows, codec,
-                        craft_oor_columns, golden_names, load, oracle,
+                        craft_dense_oor, craft_oor_columns, golden_names, load, oracle,
                         oracle_decode_blocks, oracle_encode_blocks)
 
 pytestmark = pytest.mark.gpu
@@ -410,12 +410,12 @@ def _dense_tile_setup(k, m, n_marks, P=2048, seed=99):
     return plan, dd, out, P
 
 
-@pytest.mark.parametrize("k,m", [(16, 48), (32, 32), (100, 28)])
+@pytest.mark.parametrize("k,m", [(16, 48), (32, 32)])
 def test_dense_tile_over_scratch_decodes(k, m):
     """More than kMaxTileOor (256) marks of the received rows in ONE column
     tile: the reference has no such limit, and neither does the decode --
-    the tile takes the slow bucket-walking path instead of failing (k=16:
-    matrix cores KS=1, k=32: KS=2, k=100: dot2 kernel)."""
+    the tile takes the slow path (matrix_redo_kernel) instead of failing
+    (k=16: matrix cores KS=1, k=32: KS=2, 1024- and 512-column blocks)."""
     torch = _torch()
     plan, dd, out, P = _dense_tile_setup(k, m, 600)
     cap = 1024
@@ -438,12 +438,72 @@ def test_dense_tile_over_scratch_decodes(k, m):
     assert torch.equal(dec, dd)
 
 
-@pytest.mark.parametrize("k,m", [(16, 48), (100, 28)])
+@pytest.mark.parametrize("k,m,per_col,ranges,P", [
+    # KS = 8 (256-column blocks): 2 marks per column over 4 blocks
+    (100, 28, 2, [(0, 1024)], 2048),
+    # KS = 16 (64-column blocks): 5 per column over 12 blocks -- more slow
+    # tiles than a 256-column-grain list held -- plus the dot2 tail
+    # (KP = 128, 256-column tiles) past the last whole 1024-column tile
+    (200, 56, 5, [(0, 768), (2048, 2348)], 2348),
+    (256, 768, 5, [(64, 832)], 2048),
+    # k > 256: the NTT engine walks the buckets itself (no tile list)
+    (300, 100, 5, [(0, 768)], 1024),
+])
+def test_dense_tiles_spread_decode(k, m, per_col, ranges, P):
+    """Several OOR marks in every column of many tiles (crafted by solving
+    for per_col data rows): every tile overflows the kernels' LDS mark list,
+    the slow-tile list holds one entry per tile of the narrowest block
+    width (a 256-column-grain list overflowed into the next
+    stripe's context at KS = 16) and the redo restores every mark; two
+    stripes so an overflow into the neighbour would show."""
+    torch = _torch()
+    import quadiron_amd as qa
+    rng = np.random.default_rng(k + per_col)
+    S = 2
+    data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
+    crafted = 0
+    for lo, hi in ranges:
+        crafted += craft_dense_oor(k, m, data[0], rng, range(lo, hi), range(k),
+                                   per_col)
+    assert crafted > 0.8 * sum(hi - lo for lo, hi in ranges)
+    plan = qa.Plan(k, m, False)
+    no = plan.n_outputs
+    dd = torch.from_numpy(data.view(np.int16)).cuda()
+    out = torch.zeros((S, no, P), dtype=torch.int16, device="cuda")
+    cap = 1024
+    counts = torch.zeros(S * no, dtype=torch.int32, device="cuda")
+    entries = torch.zeros(S * no * cap, dtype=torch.int32, device="cuda")
+    plan.encode(dd, out, counts, entries, cap)
+    torch.cuda.synchronize()
+    cnt = counts.cpu().numpy().reshape(S, no)
+    assert cnt.max() <= cap
+    assert cnt[0, :k].sum() >= per_col * crafted
+    ids = np.tile(np.arange(k, dtype=np.uint16), (S, 1))
+    di = torch.from_numpy(ids.view(np.int16)).cuda()
+    ctx = torch.randint(0, 256, (plan.ctx_bytes(S, P),), dtype=torch.uint8,
+                        device="cuda")
+    plan.decode_ctx(di, ctx, P, counts, entries, cap, h_ids=ids)
+    dec = torch.zeros_like(dd)
+    assert plan.decode(ctx, di, out, dec, counts=counts, entries=entries,
+                       cap=cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec, dd)
+    assert plan.take_error() == 0
+    # the same context serves a second decode (the redo emptied its lists)
+    dec.zero_()
+    assert plan.decode(ctx, di, out, dec, counts=counts, entries=entries,
+                       cap=cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec, dd)
+
+
+@pytest.mark.parametrize("k,m", [(16, 48), (100, 28), (200, 56), (300, 100)])
 def test_decode_bucket_overflow_raises(k, m):
     """A decode reading an OOR bucket whose count exceeds its capacity lost
     marks: it must raise the plan's sticky error, not return wrong data
     silently (the reference returns -1 on header overflow,
-    src/property.h:106-108)."""
+    src/property.h:106-108).  k = 16, 100, 200: matrix cores at KS = 1, 8,
+    16; k = 300: the NTT engine."""
     torch = _torch()
     plan, dd, out, P = _dense_tile_setup(k, m, 200, seed=5)
     cap = 2
