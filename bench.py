@@ -162,6 +162,31 @@ def cpu_baseline(k, m, P, systematic=False, seconds=1.0, threads=None):
             "cpu": cpu_model(), "host_cpus": os.cpu_count()}
 
 
+def pmc_record(key, stripes):
+    """profiles/pmc_roofline.json entry for a bench configuration (measured
+    at the same stripe count), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_roofline.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)["configs"].get(key)
+    except (OSError, ValueError, KeyError):
+        return None
+    if not rec or rec.get("stripes") != stripes:
+        return None
+    return dict(rec, source=rec.get("source"))
+
+
+def valu_summary(k):
+    """VALU issue of a kernel from its PMC record: SQ_INSTS_VALU per wave,
+    and the busy fraction = SQ_INSTS_VALU x 4 cycles (a wave64 int32 VALU
+    instruction issues over 4 cycles on a 16-lane SIMD) / (1024 SIMDs x the
+    launch's cycles, GRBM_GUI_ACTIVE / 8 XCDs)."""
+    if not k or not k.get("valu_instr"):
+        return None
+    return {"instr_per_wave": k.get("valu_instr_per_wave"),
+            "busy": k.get("valu_busy"), "unit": "fraction of VALU issue cycles"}
+
+
 def shard(rank, world, stripes_per_gpu):
     """Global stripe range [lo, hi) of a rank: the batch partitions by stripe
     (independent codewords), weak scaling -- no data-path collective."""
@@ -379,31 +404,25 @@ def main(argv=None):
         enc_gbs = C * enc_b / (enc_ms * 1e-3) / 1e9
         dec_gbs = C * dec_b / (dec_ms * 1e-3) / 1e9
 
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if headline and os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                traffic = json.load(f).get("encode_bytes_per_launch")
-        except Exception:
-            traffic = None
-
-    K = 1
-    while K < k:
-        K *= 2
+    # PMC record of this configuration (tools/pmc_roofline.sh: separate
+    # rocprofv3 --pmc passes over a bench run of the same shape, FETCH_SIZE
+    # doubled per MI355X_MICROARCH.md's gfx950 HBM note): HBM bytes and
+    # VALU issue per launch of the encode kernel and of the decode kernels
+    pmc = pmc_record(args.cfg + ("_sys" if sys_ else ""), S)
     name = (f"RS-FNT{'-sys' if sys_ else ''} k={k} n={n} "
             f"pkt={pkt_bytes // 1024}KiB")
     metric = ("device-resident encode+decode GB/s per GPU, RS-FNT k=16 n=64 "
               "pkt=64KiB" if headline else
               f"device-resident encode+decode GB/s per GPU, {name}")
-    # the plan's kernel choice (quadiron_amd/csrc/plan.cpp enc_matrix)
-    env_mat = os.environ.get("QI_ENC_MATRIX", "")
-    mat_enc = sys_ or (env_mat == "1" if env_mat in ("0", "1") else K == 64)
-    if k > 64:
-        enc_kernel = "ntt_lds_kernel / ntt_pass_kernel (whole encode call)"
+    # the kernels this plan launches (the library's own dispatch,
+    # qi_gpu_kernels); the dry run names the cfg2 kernels it stands in for
+    if dry:
+        kernels = "encode=encode_fnt_kernel<16,2>; decode=(dry run: none)"
     else:
-        enc_kernel = ("matrix_mfma_kernel<*>" if mat_enc
-                      else f"encode_fnt_kernel<{K},*>")
+        kernels = plan.kernels(P)
+    enc_kernel, dec_kernels = (x.split("=", 1)[1] for x in kernels.split("; "))
+    penc = (pmc or {}).get("encode") or {}
+    pdec = (pmc or {}).get("decode") or {}
     out = {
         "metric": metric,
         "value": value,
@@ -434,6 +453,9 @@ def main(argv=None):
         "decode_ms": dec_ms,
         "decode_GBps": dec_gbs,
         "roundtrip_ok": ok,
+        # the dominant kernel: the encode (one launch per encode call at
+        # every BASELINE config: whole 1024-column tiles, no tail kernel),
+        # timed by HIP events on its launch stream
         "roofline": {
             "bound": "hbm",
             "kernel": enc_kernel,
@@ -441,19 +463,41 @@ def main(argv=None):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": enc_gbs / HBM_PEAK_GBS if enc_gbs else None,
-            "traffic": traffic,
+            "traffic": penc.get("hbm_bytes_per_launch"),
             "bytes_per_launch": C * enc_b,
+            "traffic_ratio": (penc["hbm_bytes_per_launch"] / (C * enc_b)
+                              if penc.get("hbm_bytes_per_launch") else None),
+            "valu": valu_summary(penc),
         },
+        # the decode step (context build + matrix kernels) against the same
+        # roofline: algorithmic bytes 2k * 2P per stripe
+        "decode_roofline": {
+            "kernels": dec_kernels,
+            "achieved": dec_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": dec_gbs / HBM_PEAK_GBS if dec_gbs else None,
+            "traffic": pdec.get("hbm_bytes_per_launch"),
+            "bytes_per_launch": C * dec_b,
+            "traffic_ratio": (pdec["hbm_bytes_per_launch"] / (C * dec_b)
+                              if pdec.get("hbm_bytes_per_launch") else None),
+            "valu": valu_summary(pdec),
+        },
+        "pmc_source": (pmc or {}).get("source"),
         "cpu_baseline": None,
         "build_id": None if dry else qa.build_id(),
     }
     if dry:
         out["dry_run"] = True
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not dry:
+    # the CPU baseline runs on rank 0 after the timed region and its final
+    # barrier (every rank's kernels are done), at every world size, so a
+    # multi-GPU line carries the same-run CPU number as the 1-GPU one
+    if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(k, m, P, sys_, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
+        dist.barrier()  # the other ranks wait for rank 0's CPU baseline
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)

@@ -127,6 +127,12 @@ int qi_gpu_decode_packed(qi_plan* plan, const void* d_ctx,
  * their own: they are decoded by a slower path, never refused. */
 int qi_gpu_take_error(qi_plan* plan);
 
+/* Names of the kernels an encode and a decode of `words` columns launch on
+ * this plan (rows at 8-byte aligned offsets), as
+ * "encode=<kernels>; decode=<kernels>" -- diagnostics for bench lines and
+ * profiles.  The string is per calling thread, valid until its next call. */
+const char* qi_gpu_kernels(const qi_plan* plan, long long words);
+
 /* Build identification: "<git describe>+src:<hash of the library sources>". */
 const char* qi_build_id(void);
 

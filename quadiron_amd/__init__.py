@@ -56,6 +56,7 @@ def _declare(lib):
                                      I, V]),
         "qi_gpu_take_error": (I, [V]),
         "qi_build_id": (C.c_char_p, []),
+        "qi_gpu_kernels": (C.c_char_p, [V, LL]),
         "qi_fec_new": (V, [I, I, I]),
         "qi_fec_delete": (None, [V]),
         "qi_fec_n_outputs": (I, [V]),
@@ -167,6 +168,11 @@ class Plan:
             raise ValueError(f"qi_plan_create({k}, {m}, {systematic}) failed")
         self.n = lib().qi_plan_n(self.h)
         self.n_outputs = lib().qi_plan_n_outputs(self.h)
+
+    def kernels(self, words):
+        """'encode=<kernels>; decode=<kernels>' this plan launches over
+        `words` columns (qi_gpu_kernels)."""
+        return lib().qi_gpu_kernels(self.h, words).decode()
 
     def close(self):
         if self.h:

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <string>
 
 #include "fnt_codelets.h"
 #include "gf65537.h"
@@ -1947,6 +1948,37 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
     default:
         return -3;
     }
+}
+
+std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor)
+{
+    // mirrors launch_matrix_kernels / mfma_dispatch / mat_dispatch for rows
+    // at 8-byte aligned offsets inside 31-bit buffer ranges
+    std::string r;
+    const long long wfull = words / kRouteTile * kRouteTile;
+    const int KS = L.KS();
+    if (KS > 0 && wfull > 0) {
+        const int RB = L.RB();
+        int nst = KS == 1 ? 16 : 8, nw = 4;
+        bool rsplit = RB >= 4;
+        if (KS == 16) {
+            nst = 1;
+            rsplit = true;
+        } else if (KS == 8) {
+            nst = 4;
+            rsplit = true;
+        }
+        r = "matrix_mfma_kernel<" + std::to_string(KS) + "," + std::to_string(nst) + "," +
+            std::to_string(nw) + "," + (rsplit ? "true" : "false") + ">";
+    }
+    if (wfull < words) {
+        const int cols = L.KP <= 8 ? 4 : L.KP <= 16 ? 2 : 1;
+        r += std::string(r.empty() ? "" : " + ") + "matrix_kernel<" + std::to_string(L.KP) +
+             "," + std::to_string(cols) + ",true> (tail)";
+    }
+    if (in_oor)
+        r += " + matrix_redo_kernel";
+    return r;
 }
 
 int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,

@@ -1020,6 +1020,12 @@ int ntt_plan_init(qi_plan* p)
     return 0;
 }
 
+const char* ntt_engine_name(const qi_plan* p)
+{
+    return lds_engine(p) ? "ntt_lds_kernel"
+                         : "ntt_pass_kernel (+ ntt_expand_kernel / ntt_fix_kernel)";
+}
+
 void ntt_plan_free(qi_plan* p)
 {
     if (p->d_tw[0])

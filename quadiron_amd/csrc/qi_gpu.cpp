@@ -2,6 +2,7 @@
 // device-resident stripes.
 #include <hip/hip_runtime.h>
 
+#include <string>
 #include <vector>
 
 #include "../../include/qi_gpu.h"
@@ -199,6 +200,32 @@ int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
                          n_stripes, d_counts ? &in : nullptr, 0, nullptr, p->d_rowid,
                          reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
                          cs, ctx_slow(p, d_ctx, words), p->d_err, st(stream));
+}
+
+const char* qi_gpu_kernels(const qi_plan* p, long long words)
+{
+    static thread_local std::string names;
+    if (!p || words <= 0)
+        return "";
+    std::string enc, dec;
+    if (p->ntt) {
+        enc = ntt_engine_name(p);
+        dec = std::string("ntt_ctx_kernel + ") + ntt_engine_name(p);
+    } else {
+        if (!p->d_gen) {
+            enc = "encode_fnt_kernel<" + std::to_string(p->K) + "," +
+                  std::to_string(p->K <= 16 ? 2 : 1) + ">";
+        } else {
+            enc = matrix_kernel_names(p->gen, words, false);
+        }
+        const MatLayout L = ctx_layout(p);
+        dec = std::string(p->k > 128 ? "decode_ctx_kernel<1024,true>"
+                          : p->k > 32 ? "decode_ctx_kernel<256,false>"
+                                      : "decode_ctx_kernel<64,false>") +
+              " + " + matrix_kernel_names(L, words, true);
+    }
+    names = "encode=" + enc + "; decode=" + dec;
+    return names.c_str();
 }
 
 // git describe of the tree the library was built from + a hash of its

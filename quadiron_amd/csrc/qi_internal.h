@@ -6,6 +6,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
 #include <vector>
 
 #include "matrix_pack.h"  // MatLayout: the packed matrix block
@@ -122,6 +123,9 @@ int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
 
 // matrix kernel instantiation choice
 int matrix_kp(int kin);
+// names of the kernels launch_matrix runs for L over `words` columns
+// (aligned rows; diagnostics: qi_gpu_kernels)
+std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor);
 
 // ---- host math (plan.cpp) ----
 // Lagrange matrix for points x_i = r^{ids[i]}:

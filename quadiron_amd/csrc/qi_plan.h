@@ -93,6 +93,8 @@ struct qi_plan {
 namespace qi {
 // ---- general-k path (ntt.hip) ----
 int ntt_plan_init(qi_plan* p);
+// "ntt_lds_kernel" (max(n, len_2k) <= 2048) or the multi-pass engine
+const char* ntt_engine_name(const qi_plan* p);
 void ntt_plan_free(qi_plan* p);
 long long ntt_ctx_words(const qi_plan* p);
 int ntt_build_ctx(const qi_plan* p, const uint16_t* d_ids, int n_stripes, int32_t* d_ctx,

@@ -230,6 +230,13 @@ def main():
     # k > 256: the NTT-structured path (k <= 256 moved to the matrix cores)
     gen_blocks(ref, ora, "blk_k300_m212", 300, 212, 0, 128, 600 + 2, 37, 2, 8, out)
     gen_blocks(ref, ora, "blk_k260_m30_sys", 260, 30, 1, 256, 512, 38, 2, 8, out)
+    # max(n, len_2k) > 2048: the multi-pass NTT engine (ntt_pass_kernel over
+    # HBM scratch) -- n = 4096 non-systematic and systematic, len_2k = 4096
+    # > n = 2048, and n = 16384 (round 3)
+    gen_blocks(ref, ora, "blk_k300_m3796", 300, 3796, 0, 64, 256 + 2, 39, 2, 8, out)
+    gen_blocks(ref, ora, "blk_k260_m3000_sys", 260, 3000, 1, 128, 256, 40, 2, 8, out)
+    gen_blocks(ref, ora, "blk_k1100_m100", 1100, 100, 0, 64, 256 + 6, 41, 2, 8, out)
+    gen_blocks(ref, ora, "blk_k300_m16000", 300, 16000, 0, 32, 64 + 2, 42, 1, 8, out)
 
 
 if __name__ == "__main__":

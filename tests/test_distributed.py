@@ -78,7 +78,8 @@ def test_bench_launches_n_ranks(n):
     """`bench.py --gpus N` (no launcher around it) starts N ranks itself
     before anything touches HIP, and rank 0 reports the process group's
     size -- the dry run takes the same launch/shard/reduce path on gloo."""
-    r = _bench(["--gpus", str(n), "--dry-run", "--steps", "2", "--warmup", "1"])
+    r = _bench(["--gpus", str(n), "--dry-run", "--steps", "2", "--warmup", "1",
+                "--cpu-seconds", "0.2"])
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only
@@ -90,6 +91,11 @@ def test_bench_launches_n_ranks(n):
     per = (16 + 64) * 2 * 32768 + 2 * 16 * 2 * 32768
     assert out["value"] == pytest.approx(
         n * 4096 * 2 * per / (out["ms_per_step"] * 2e-3) / 1e9, rel=1e-6)
+    # the same-run CPU baseline rides on every world size (rank 0, after the
+    # timed region and the final barrier)
+    cb = out["cpu_baseline"]
+    assert cb is not None and cb["value"] > 0 and cb["cores"] >= 1
+    assert cb["kind"] in ("reference", "port")
 
 
 def test_bench_world_mismatch_fails():
