@@ -1,0 +1,863 @@
+// Per-stripe decode contexts on the GPU for the matrix paths (k <= 256):
+// the Lagrange form of DecodeContext::init (src/fec_context.h:232-274), the
+// packed / matrix-core forms of the interpolation matrix (matrix_pack.h)
+// and the OOR route tables of decode_prepare (src/fec_base.h:1361-1404).
+#include <hip/hip_runtime.h>
+
+#include "gf65537.h"
+#include "matrix_pack.h"
+#include "qi_internal.h"
+
+// timing probes only (QI_PROBE_SKIP bits skip context phases; results wrong)
+#ifndef QI_PROBE_SKIP
+#define QI_PROBE_SKIP 0
+#endif
+
+// timestamp probe (QI_PROBE_TS builds only): per workgroup, s_memrealtime
+// (100 MHz) at the phase boundaries of decode_ctx_lds_kernel, read back by
+// qi_probe_read (tools/ctx_ts.py)
+#ifdef QI_PROBE_TS
+__device__ unsigned long long qi_probe_ts[8192][8];
+extern "C" int qi_probe_read(void* host, size_t bytes)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(qi_probe_ts), bytes) == hipSuccess ? 0 : -1;
+}
+#define QI_TS(n)                                                                    \
+    do {                                                                            \
+        if (threadIdx.x == 0)                                                       \
+            qi_probe_ts[blockIdx.x & 8191][n] = __builtin_amdgcn_s_memrealtime();   \
+    } while (0)
+#else
+#define QI_TS(n) ((void)0)
+#endif
+
+namespace qi {
+// ---------------------------------------------------------------------------
+// Per-stripe decode context: the Lagrange form of DecodeContext::init
+// (src/fec_context.h:232-274).  For received points x_i = r^{id_i}:
+//   A(x) = prod_j (x - x_j),  Q_i = A / (x - x_i),  A'(x_i) = Q_i(x_i)
+//   mode 0: M[t][i] = coef_t(Q_i) / A'(x_i)       (non-systematic)
+//   mode 1: M[t][i] = Q_i(r^t)   / A'(x_i)        (systematic)
+// plus the OOR route table of the stripe (decode_prepare's props walk,
+// src/fec_base.h:1361-1404, precomputed per tile).
+// One workgroup per stripe (64 lanes for k <= 32, else 256); k <= 256.
+// ---------------------------------------------------------------------------
+// canonical a * b mod 65537 for a, b in [0, 65536]: with 2^16 = -1 and
+// 2^32 = 1, p = p0 + p1 2^16 + p2 2^32 reduces to p0 - p1 + p2
+__device__ __forceinline__ uint32_t mulm(uint32_t a, uint32_t b)
+{
+    // balanced operands (|a|, |b| <= 32768): the product fits int32 and one
+    // full-rate v_mul_i32_i24 forms it (the 64-bit product took two
+    // quarter-rate v_mul_{lo,hi}_u32 on the serial Lagrange chains)
+    const int32_t ab = static_cast<int32_t>(a) - (a > 32768u ? 65537 : 0);
+    const int32_t bb = static_cast<int32_t>(b) - (b > 32768u ? 65537 : 0);
+    const int32_t p = __mul24(ab, bb);                      // |p| <= 2^30
+    const int32_t v = (p & 0xffff) - (p >> 16);             // [-16384, 81919]
+    const int32_t w = v < 0 ? v + 65537 : v;                // [0, 81919]
+    return static_cast<uint32_t>(w >= 65537 ? w - 65537 : w);
+}
+__device__ __forceinline__ uint32_t addm(uint32_t a, uint32_t b)
+{
+    const uint32_t c = a + b;
+    return c >= 65537u ? c - 65537u : c;
+}
+__device__ __forceinline__ uint32_t subm(uint32_t a, uint32_t b)
+{
+    return a >= b ? a - b : a + 65537u - b;
+}
+__device__ __forceinline__ uint32_t powm(uint32_t b, uint32_t e)
+{
+    uint32_t r = 1;
+    for (; e; e >>= 1) {
+        if (e & 1)
+            r = mulm(r, b);
+        b = mulm(b, b);
+    }
+    return r;
+}
+
+// NT threads: the Lagrange part runs on the first wave (lane = point); the
+// row packing and the MFMA operand tiles use every thread (NT = 256 for
+// k > 32, where they dominate and there are few stripes per launch).
+// pack_row (matrix_pack.h) on a group of LPR adjacent lanes (a power of 2,
+// <= 16), lane `sub` taking entries sub, sub + LPR, ...: the column scale
+// 1 / A'(x_i) applied, the same row scale search (uniform in the group),
+// packed pairs, canonical `plain` entries, kcorr / rscale / kmf, and the
+// row-scaled entries written back to the LDS row for the tiles.  Entries
+// lane-fastest: a group's global stores are runs of LPR dwords (4 lanes per
+// row with 16-byte runs took 17 of the 43 us of a k = 64 context).
+__device__ __forceinline__ uint32_t grp_or(uint32_t v, int lpr)
+{
+    for (int m = 1; m < lpr; m <<= 1)
+        v |= __shfl_xor(v, m, lpr);
+    return v;
+}
+__device__ __forceinline__ uint32_t grp_add(uint32_t v, int lpr)
+{
+    for (int m = 1; m < lpr; m <<= 1)
+        v += __shfl_xor(v, m, lpr);
+    return v;
+}
+__device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLayout& L,
+                             int t, int32_t* block, int sub, int lpr)
+{
+    // the lane's entries i = sub + m lpr (m < 16: k <= 256 at lpr = 16) in
+    // registers: every row load is issued up front (rows in global memory
+    // for k > 128), and the packed pairs take the odd entry from the
+    // neighbour lane by shuffle instead of re-reading the row
+    constexpr int ME = 16;
+    const int kin = L.kin, KP = L.KP;
+    uint32_t v[ME];
+#pragma unroll
+    for (int m = 0; m < ME; m++) {
+        const int i = sub + m * lpr;
+        v[m] = i < kin ? row[i] : 0u;
+    }
+    uint32_t bad = 0;
+#pragma unroll
+    for (int m = 0; m < ME; m++) {
+        const int i = sub + m * lpr;
+        if (i < kin) {
+            v[m] = mulm(v[m], cscale[i]);
+            bad |= !coef_ok(balanced(v[m]));
+        }
+    }
+    bad = grp_or(bad, lpr);
+    uint32_t s = 1;
+    while (bad) {  // rare; s, si and bad are uniform in the group
+        s++;
+        const int32_t si = balanced(powm(s, 65535u));
+        if (iabs32(si) > 32766)
+            continue;
+        bad = 0;
+#pragma unroll
+        for (int m = 0; m < ME; m++) {
+            const int i = sub + m * lpr;
+            if (i < kin)
+                bad |= !coef_ok(balanced(mulm(v[m], s)));
+        }
+        bad = grp_or(bad, lpr);
+    }
+    int32_t* packed = block + static_cast<size_t>(t) * KP;
+    int32_t* plain = block + L.plain();
+    uint32_t sum = 0;  // <= 256 * 65536 = 2^24
+#pragma unroll
+    for (int m = 0; m < ME; m++) {
+        const int i = sub + m * lpr;
+        if (s != 1 && i < kin)
+            v[m] = mulm(v[m], s);
+        // pair (i, i + 1) for even i: the odd entry sits on lane sub + 1
+        const uint32_t odd = __shfl_xor(v[m], 1, lpr);
+        if (i < kin) {
+            row[i] = v[m];
+#ifndef QI_PROBE_NOPLAIN
+            plain[static_cast<size_t>(t) * kin + i] = static_cast<int32_t>(v[m]);
+#endif
+            sum += v[m];
+#ifndef QI_PROBE_NOPACKED
+            if (!(sub & 1)) {
+#else
+            if (false) {
+#endif
+                const int32_t lo = balanced(v[m]);
+                const int32_t hi = i + 1 < kin ? balanced(odd) : 0;
+                packed[i >> 1] = static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xffffu) |
+                                                      (static_cast<uint32_t>(hi) << 16));
+            }
+        }
+    }
+    // pairs past kin up to KP stay zero (the dot2 kernel's padding)
+#ifndef QI_PROBE_NOPACKED
+    for (int j = (kin + 1) / 2 + sub; j < KP; j += lpr)
+        packed[j] = 0;
+#endif
+    sum = grp_add(sum, lpr);
+    if (sub == 0) {
+        // sum mod q by two folds (2^16 = -1), then canonical
+        int32_t f = static_cast<int32_t>(sum & 0xffffu) - static_cast<int32_t>(sum >> 16);
+        f = f < 0 ? f + 65537 : f;
+        const uint32_t sq = static_cast<uint32_t>(f >= 65537 ? f - 65537 : f);
+        block[L.kcorr() + t] = static_cast<int32_t>(mulm(sq, 32768u));
+        block[L.rscale() + t] = s == 1 ? 1 : balanced(powm(s, 65535u));
+        if (L.KS()) {
+            block[L.kmf() + t] = static_cast<int32_t>(mulm(sq, 32896u));
+            block[L.rscale_mf() + t] = block[L.rscale() + t];
+        }
+    }
+}
+
+// LDS row pitch of the context kernel's k x k matrix: 4 x odd, >= k
+__host__ __device__ inline int ctx_pitch(int k)
+{
+    return (k + 3) / 8 * 8 + 4;
+}
+
+template <int NT, bool BIG>
+__global__ __launch_bounds__(NT) void decode_ctx_kernel(
+    int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
+    int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
+    int by_pos, long long words, uint32_t* err)
+{
+    __shared__ uint32_t xs[256];
+    __shared__ uint32_t A[257];
+    __shared__ uint32_t cinv[256];    // 1 / A'(x_i)
+    __shared__ uint32_t aprime[256];  // A'(x_i)
+    // k x k matrix, sized by the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
+    // limited the kernel to 4 workgroups per CU
+    extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
+    // row pitch = 4 x odd (>= k, a multiple of 4 words): the tile pass
+    // reads 16 rows x 16 bytes per wave (ds_read_b128) conflict-free (the
+    // odd pitch k | 1 had SQ_LDS_BANK_CONFLICT at 7.4 cycles per LDS
+    // instruction at k = 64)
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x;
+    int32_t* mat = ctx + s * ctx_stride;
+    // BIG (128 < k <= 256): the k x k matrix (up to 256 KB) does not fit
+    // LDS; its rows live in the context's own `plain` section (pitch k),
+    // which the packing pass rewrites in place with the row-scaled entries
+    const int kp = BIG ? k : ctx_pitch(k);
+    uint32_t* Mt = BIG ? reinterpret_cast<uint32_t*>(mat + L.plain()) : qi_ctx_lds;
+    int32_t* cids = mat + L.words();
+    uint32_t* route = reinterpret_cast<uint32_t*>(cids + 2 * L.KP);
+    for (int i = k + tid; i < 2 * L.KP; i += NT)
+        cids[i] = 0;
+    const long long ntiles = route_tiles(words);
+
+    // route table: clear, then (after the barrier below) fill; the
+    // slow-tile list behind it starts empty
+    for (long long t = tid; t < ntiles; t += NT)
+        route[t * kRouteStride] = 0;
+    if (tid == 0)
+        route[ntiles * kRouteStride] = 0;
+    if (tid < k) {
+        const uint32_t id = ids[static_cast<long long>(s) * k + tid];
+        xs[tid] = (QI_PROBE_SKIP & 32) ? id + 2 : powm(r, id);
+        cids[tid] = static_cast<int32_t>(id);
+    }
+    __syncthreads();
+    if (!(QI_PROBE_SKIP & 1) && in_oor.counts && tid < k) {
+        const int id = ids[static_cast<long long>(s) * k + tid];
+        const int slot = (by_pos ? tid : id) - slot_base;
+        if (slot >= 0) {
+            const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
+            uint32_t c = in_oor.counts[bk];
+            if (c > static_cast<uint32_t>(in_oor.cap)) {
+                atomicOr(err, kErrOorTruncated);
+                c = static_cast<uint32_t>(in_oor.cap);
+            }
+            for (uint32_t e = 0; e < c; e++) {
+                const uint32_t w = in_oor.entries[bk * in_oor.cap + e];
+                if (w >= words)
+                    continue;
+                uint32_t* rt = route + (w / kRouteTile) * kRouteStride;
+                const uint32_t p = atomicAdd(rt, 1u);
+                if (p < static_cast<uint32_t>(kRouteCap))
+                    rt[1 + p] = (static_cast<uint32_t>(tid) << 16) | (w % kRouteTile);
+            }
+        }
+    }
+    // A(x) = prod_i (x - x_i), lane d holding coefficient d (and d + 64,
+    // d + 128, ... for k > 64).  A is monic: A[k] = 1 is set explicitly, so
+    // k = 64 (128, 256) needs no 65th (129th, 257th) coefficient slot.
+    if (!(QI_PROBE_SKIP & 2) && tid < 64) {  // wave 0 (wave-uniform)
+        uint32_t a = tid == 0 ? 1u : 0u;
+        if (k <= 64) {
+            for (int i = 0; i < k; i++) {
+                uint32_t prev = __shfl_up(a, 1);
+                if (tid == 0)
+                    prev = 0;
+                a = subm(prev, mulm(xs[i], a));
+            }
+        } else {
+            // slot u holds coefficient 64 u + lane (u < nslot <= 4)
+            const int nslot = (k + 63) / 64;
+            uint32_t au[4] = {a, 0u, 0u, 0u};
+            for (int i = 0; i < k; i++) {
+                uint32_t prev[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    prev[u] = __shfl_up(au[u], 1);
+#pragma unroll
+                for (int u = 1; u < 4; u++) {
+                    const uint32_t top = __shfl(au[u - 1], 63);  // 64 u - 1 -> 64 u
+                    if (tid == 0)
+                        prev[u] = top;
+                }
+                if (tid == 0)
+                    prev[0] = 0;
+                const uint32_t x = xs[i];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (u < nslot)
+                        au[u] = subm(prev[u], mulm(x, au[u]));
+            }
+            a = au[0];
+#pragma unroll
+            for (int u = 1; u < 4; u++)
+                if (u < nslot)
+                    A[64 * u + tid] = au[u];
+        }
+        A[tid] = a;
+        if (tid == 0)
+            A[k] = 1;
+    }
+    __syncthreads();
+    if (!(QI_PROBE_SKIP & 4) && tid < k) {
+        // Q_i = A / (x - x_i) by synthetic division from the top, and
+        // A'(x_i) = Q_i(x_i) by Horner over the same coefficients (two
+        // interleaved chains; the product prod_{j != i} (x_i - x_j) was a
+        // third serial chain).  The rows hold the unscaled values; the
+        // column scale 1 / A'(x_i) is applied by the packing pass.
+        const uint32_t xi = xs[tid];
+        uint32_t q = 1, h = 1;  // A[k]; Q_i(x_i) so far
+        if (mode == 0)
+            Mt[(k - 1) * kp + tid] = 1;
+        for (int j = k - 1; j >= 1; j--) {
+            q = addm(A[j], mulm(xi, q));
+            if (mode == 0)
+                Mt[(j - 1) * kp + tid] = q;
+            h = addm(mulm(h, xi), q);
+        }
+        aprime[tid] = h;
+        cinv[tid] = powm(h, 65535u);
+    }
+    if (mode != 0) {
+        // systematic: M[t][i] = Q_i(r^t) / A'(x_i), one thread per row t,
+        // with Q_i(r^t) = A(r^t) / (r^t - x_i): 0 when r^t is another
+        // received point (A(r^t) = 0), A'(x_i) when it is x_i itself.  The
+        // k inverses of a row come from one inversion (prefix products, the
+        // running inverse walked back), so a row costs ~3k + 24 serial
+        // multiplies (Horner of every Q_i at every r^t took k^2 per lane).
+        __syncthreads();
+        if (tid < k) {
+            uint32_t* row = Mt + tid * kp;
+            const uint32_t et = powm(r, static_cast<uint32_t>(tid));
+            uint32_t av = 1;  // A(r^t), A monic
+            for (int j = k - 1; j >= 0; j--)
+                av = addm(mulm(av, et), A[j]);
+            uint32_t pre = 1;
+            for (int i = 0; i < k; i++) {
+                const uint32_t d = subm(et, xs[i]);
+                row[i] = pre;
+                pre = mulm(pre, d ? d : 1u);
+            }
+            uint32_t inv = powm(pre, 65535u);
+            for (int i = k - 1; i >= 0; i--) {
+                const uint32_t d = subm(et, xs[i]);
+                const uint32_t inv_i = mulm(inv, row[i]);
+                inv = mulm(inv, d ? d : 1u);
+                row[i] = d ? mulm(av, inv_i) : aprime[i];
+            }
+        }
+    }
+    __syncthreads();
+    {
+        // LPR lanes per row: 4 entries per lane at k = 64
+        const int q4 = (k + 3) / 4;
+        const int lpr = q4 <= 4 ? 4 : q4 <= 8 ? 8 : 16;
+        for (int t = tid / lpr; !(QI_PROBE_SKIP & 8) && t < L.R; t += NT / lpr)
+            pack_row_grp(Mt + t * kp, cinv, L, t, mat, tid & (lpr - 1), lpr);
+    }
+    if (!(QI_PROBE_SKIP & 16) && L.KS()) {
+        // the matrix-core operand tiles, from the row-scaled entries in LDS
+        __syncthreads();
+        // per (row t, 4 consecutive entries): split once, then place the
+        // a / b byte words in their tile dwords (pack_mf_dword's layout;
+        // rows t >= R are zero).  Items run row-fastest, so 16 lanes read
+        // 16 rows' entries i0..i0+3 (one ds_read_b128 each) and a wave's
+        // stores cover whole 128-byte tile lines (16 rows x 2 dwords).  At
+        // KS >= 4 the zero halves of [a | 0] and [0 | b] are not written:
+        // matrix_mfma_kernel skips those K-steps (and never loads them).
+        const int KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
+        int32_t* mf = mat + L.mf();
+        // BIG: the rows come from global memory; 4 items per thread have
+        // their loads in flight together (the stores to the tiles may alias
+        // the rows as far as the compiler knows, so it would not overlap
+        // the iterations itself)
+        constexpr int IB = BIG ? 4 : 1;
+        const int items = RB * nj * 16;
+        for (int it0 = tid; it0 < items; it0 += IB * NT) {
+            uint32_t e[IB][4];
+#pragma unroll
+            for (int ib = 0; ib < IB; ib++) {
+                const int it = it0 + ib * NT;
+                const int tl4 = it & 15, jj = it >> 4;
+                const int t = 16 * (jj / nj) + tl4, i0 = 4 * (jj % nj);
+                const bool live = it < items && t < L.R && i0 < k;
+                if constexpr (BIG) {  // global rows, pitch k: no 16-byte alignment
+#pragma unroll
+                    for (int jb = 0; jb < 4; jb++)
+                        e[ib][jb] = live && i0 + jb < k ? Mt[t * kp + i0 + jb] : 0u;
+                } else if (live) {
+                    const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
+                    e[ib][0] = e4.x;
+                    e[ib][1] = e4.y;
+                    e[ib][2] = e4.z;
+                    e[ib][3] = e4.w;
+                }
+            }
+#pragma unroll
+            for (int ib = 0; ib < IB; ib++) {
+                const int it = it0 + ib * NT;
+                if (it >= items)
+                    break;
+                const int tl4 = it & 15, jj = it >> 4;
+                const int j = jj % nj, rb = jj / nj;
+                const int t = 16 * rb + tl4, i0 = 4 * j;
+                uint32_t aw = 0, bw = 0;
+                if (t < L.R && i0 < k) {
+#pragma unroll
+                    for (int jb = 0; jb < 4; jb++) {
+                        if (i0 + jb < k) {
+                            int32_t a, b;
+                            split_i8(e[ib][jb], a, b);
+                            aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
+                            bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int half = 0; half < 2; half++) {
+                    const int K = half * KH + i0;
+                    const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
+                    const size_t base =
+                        static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl4) * 2 + dw;
+                    if (KS < 4 || half == 0)
+                        mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
+                    if (KS < 4 || half == 1)
+                        mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
+                    mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k <= 128: the whole context in LDS, every serial chain short and lazy.
+//   - x_i = r^{id_i} from the plan's power table (one load, no powm chain);
+//   - A(x) on wave 0, one coefficient (two for k > 64) per lane, the shift
+//     by DPP (wave_shr:1) and the product x_i a_j as mul_rt (48-bit product,
+//     2^32 = 1 and 2^16 = -1) folded once per step: no canonical reductions
+//     on the chain; the route table is filled by the other waves meanwhile;
+//   - Q_i and A'(x_i) by the same lazy Horner chains (q, h stay below 2^18);
+//     1 / A'(x_i) by a 19-multiply addition chain of x^(2^16 - 1);
+//   - the column scale, the row-scale test, the row sums, the operand tiles
+//     and the plain / packed rows in item passes (thread = 4 entries of one
+//     row, rows fastest), with the rare row rescale done by one lane.
+// The round-2 kernel spent 23 of its 47 us (k = 64) in its row packing
+// (shuffle reductions per row group) and 14 in the A(x) / Q chains
+// (ds_bpermute shifts, canonical mulm at every step).
+// ---------------------------------------------------------------------------
+// x * y mod q for |x|, |y| < 2^17: the 48-bit product as v_mul_i32_i24 +
+// v_mul_hi_i32_i24, reduced with 2^32 = 1 and 2^16 = -1: |result| < 65600
+__device__ __forceinline__ int32_t mul_lz(int32_t x, int32_t y)
+{
+    uint32_t lo;
+    int32_t hi;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(lo) : "v"(x), "v"(y));
+    asm("v_mul_hi_i32_i24 %0, %1, %2" : "=v"(hi) : "v"(x), "v"(y));
+    return static_cast<int32_t>(lo & 0xffffu) - static_cast<int32_t>(lo >> 16) + hi;
+}
+
+// canonical residue of |y| < 98305 (fold -> [-2, 65537], then +-q)
+__device__ __forceinline__ uint32_t canon_lz(int32_t y)
+{
+    const int32_t f = fold(y);
+    const int32_t c = f < 0 ? f + 65537 : f;
+    return static_cast<uint32_t>(c >= 65537 ? c - 65537 : c);
+}
+
+// x^(2^16 - 1) = x^-1 (x != 0) by the chain x^(2^2-1), x^(2^4-1),
+// x^(2^8-1), x^(2^16-1): 15 squarings + 4 multiplies, all lazy
+__device__ __forceinline__ uint32_t inv_lz(uint32_t xc)
+{
+    const int32_t x = balanced(xc);
+    const int32_t e2 = mul_lz(mul_lz(x, x), x);        // x^3
+    int32_t t = mul_lz(e2, e2);
+    t = mul_lz(t, t);                                  // x^12
+    const int32_t e4 = mul_lz(t, e2);                  // x^15
+    t = e4;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        t = mul_lz(t, t);
+    const int32_t e8 = mul_lz(t, e4);                  // x^255
+    t = e8;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        t = mul_lz(t, t);
+    return canon_lz(mul_lz(t, e8));                    // x^65535
+}
+
+// entries a row may hold (coef_ok on a canonical residue): the dot2 kernel
+// needs |balanced| <= 32766, the i8 split anything but 32640
+__device__ __forceinline__ bool coef_bad(uint32_t e)
+{
+    return e - 32767u < 4u || e == 32640u;
+}
+
+// r^(2^b), balanced, b < 16: x = r^id by at most log2(n) multiplies
+struct RPow2 {
+    int32_t v[16];
+};
+
+__device__ __forceinline__ int32_t rpow_lz(const RPow2& rp, uint32_t e, int lgn)
+{
+    int32_t acc = 1;
+    for (int b = 0; b < lgn; b++)
+        acc = (e >> b) & 1u ? mul_lz(acc, rp.v[b]) : acc;
+    return acc;  // lazy, |acc| < 65600
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
+    int k, RPow2 rp, int lgn, int mode, MatLayout L,
+    const uint16_t* __restrict__ ids, int32_t* __restrict__ ctx, long long ctx_stride,
+    Oor in_oor, int slot_base, int by_pos, long long words, uint32_t* err)
+{
+    __shared__ uint32_t xs[128];
+    __shared__ int32_t A[129];        // balanced coefficients of A(x)
+    __shared__ __attribute__((aligned(16))) uint32_t cinv[128];  // 1 / A'(x_i)
+    __shared__ uint32_t aprime[128];  // A'(x_i)
+    extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x;
+    QI_TS(0);
+    int32_t* mat = ctx + s * ctx_stride;
+    const int kp = ctx_pitch(k);
+    uint32_t* Mt = qi_ctx_lds;
+    int32_t* cids = mat + L.words();
+    uint32_t* route = reinterpret_cast<uint32_t*>(cids + 2 * L.KP);
+    const long long ntiles = route_tiles(words);
+
+    for (int i = k + tid; i < 2 * L.KP; i += NT)
+        cids[i] = 0;
+    for (long long t = tid; t < ntiles; t += NT)
+        route[t * kRouteStride] = 0;
+    if (tid == 0)
+        route[ntiles * kRouteStride] = 0;  // the slow-tile list starts empty
+    // x_i = r^{id_i}: thread tid takes point tid (its Q chain below); wave 0
+    // also point 64 + lane (its A(x) chain reads every point by readlane)
+    int32_t xt = 0, xt1 = 0;
+    if (tid < k) {
+        const uint32_t id = ids[static_cast<long long>(s) * k + tid];
+        xt = balanced(canon_lz(rpow_lz(rp, id, lgn)));
+        xs[tid] = static_cast<uint32_t>(xt < 0 ? xt + kQ : xt);
+        cids[tid] = static_cast<int32_t>(id);
+    }
+    if (tid < 64 && 64 + tid < k)
+        xt1 = balanced(canon_lz(rpow_lz(rp, ids[static_cast<long long>(s) * k + 64 + tid], lgn)));
+    QI_TS(1);
+    int32_t ab0 = 0;  // wave 0: balanced A[lane] (k <= 64), for the Q chains
+    if (tid < 64) {
+        // A(x) = prod_i (x - x_i): lane d holds coefficient d (a0) and
+        // 64 + d (a1, k > 64); A is monic, A[k] = 1 set below.  x_i by
+        // readlane (no LDS round trip on the chain)
+        int32_t a0 = tid == 0 ? 1 : 0, a1 = 0;
+        if (k <= 64) {
+            for (int i = 0; i < k; i++) {
+                const int32_t x = __builtin_amdgcn_readlane(xt, i);
+                const int32_t prev = __builtin_amdgcn_update_dpp(0, a0, 0x138, 0xf, 0xf, false);
+                a0 = fold(prev - mul_lz(a0, x));
+            }
+        } else {
+            for (int i = 0; i < k; i++) {
+                const int32_t x = i < 64 ? __builtin_amdgcn_readlane(xt, i)
+                                         : __builtin_amdgcn_readlane(xt1, i - 64);
+                const int32_t top = __builtin_amdgcn_readlane(a0, 63);
+                const int32_t p0 = __builtin_amdgcn_update_dpp(0, a0, 0x138, 0xf, 0xf, false);
+                int32_t p1 = __builtin_amdgcn_update_dpp(0, a1, 0x138, 0xf, 0xf, false);
+                p1 = tid == 0 ? top : p1;
+                a0 = fold(p0 - mul_lz(a0, x));
+                a1 = fold(p1 - mul_lz(a1, x));
+            }
+            if (64 + tid < k)
+                A[64 + tid] = balanced(canon_lz(a1));
+        }
+        ab0 = balanced(canon_lz(a0));
+        if (tid < k)
+            A[tid] = ab0;
+        if (tid == 0)
+            A[k] = 1;
+    } else if (in_oor.counts) {
+        // route the received rows' OOR marks into per-tile tables (the
+        // other waves, while wave 0 builds A(x))
+        for (int i = tid - 64; i < k; i += NT - 64) {
+            const int id = ids[static_cast<long long>(s) * k + i];
+            const int slot = (by_pos ? i : id) - slot_base;
+            if (slot < 0)
+                continue;
+            const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
+            uint32_t c = in_oor.counts[bk];
+            if (c > static_cast<uint32_t>(in_oor.cap)) {
+                atomicOr(err, kErrOorTruncated);
+                c = static_cast<uint32_t>(in_oor.cap);
+            }
+            for (uint32_t e = 0; e < c; e++) {
+                const uint32_t w = in_oor.entries[bk * in_oor.cap + e];
+                if (w >= words)
+                    continue;
+                uint32_t* rt = route + (w / kRouteTile) * kRouteStride;
+                const uint32_t p = atomicAdd(rt, 1u);
+                if (p < static_cast<uint32_t>(kRouteCap))
+                    rt[1 + p] = (static_cast<uint32_t>(i) << 16) | (w % kRouteTile);
+            }
+        }
+    }
+    __syncthreads();
+    QI_TS(2);
+    if (tid < k) {
+        // Q_i = A / (x - x_i) by synthetic division from the top, and
+        // A'(x_i) = Q_i(x_i) by Horner beside it; lazy: |q| < 98400,
+        // |h| < 2^18 (the rows keep the lazy q, scaled and made canonical
+        // by the item pass).  k <= 64: A[j] by readlane from wave 0's
+        // registers
+        const int32_t x = xt;
+        int32_t q = 1, h = 1;
+        if (mode == 0)
+            Mt[(k - 1) * kp + tid] = 1;
+        if (k <= 64) {
+            for (int j = k - 1; j >= 1; j--) {
+                q = __builtin_amdgcn_readlane(ab0, j) + mul_lz(q, x);
+                if (mode == 0)
+                    Mt[(j - 1) * kp + tid] = static_cast<uint32_t>(q);
+                h = q + mul_lz(h, x);
+            }
+        } else {
+            for (int j = k - 1; j >= 1; j--) {
+                q = A[j] + mul_lz(q, x);
+                if (mode == 0)
+                    Mt[(j - 1) * kp + tid] = static_cast<uint32_t>(q);
+                h = q + mul_lz(h, x);
+            }
+        }
+        const uint32_t ap = canon_lz(fold(h));
+        aprime[tid] = ap;
+        cinv[tid] = inv_lz(ap);
+    }
+    if (mode != 0) {
+        // systematic: M[t][i] = Q_i(r^t) / A'(x_i), one thread per row t,
+        // Q_i(r^t) = A(r^t) / (r^t - x_i) (0 when r^t is another received
+        // point, A'(x_i) when it is x_i), the k inverses of a row from one
+        // inversion (prefix products walked back)
+        __syncthreads();
+        if (tid < k) {
+            uint32_t* row = Mt + tid * kp;
+            const uint32_t et = canon_lz(rpow_lz(rp, static_cast<uint32_t>(tid), lgn));
+            uint32_t av = 1;  // A(r^t), A monic
+            for (int j = k - 1; j >= 0; j--)
+                av = canon_lz(fold(mul_lz(balanced(av), balanced(et)) + A[j]));
+            uint32_t pre = 1;
+            for (int i = 0; i < k; i++) {
+                const uint32_t d = et >= xs[i] ? et - xs[i] : et + 65537u - xs[i];
+                row[i] = pre;
+                pre = canon_lz(mul_lz(balanced(pre), balanced(d ? d : 1u)));
+            }
+            uint32_t inv = inv_lz(pre);
+            for (int i = k - 1; i >= 0; i--) {
+                const uint32_t d = et >= xs[i] ? et - xs[i] : et + 65537u - xs[i];
+                const uint32_t inv_i = canon_lz(mul_lz(balanced(inv), balanced(row[i])));
+                inv = canon_lz(mul_lz(balanced(inv), balanced(d ? d : 1u)));
+                row[i] = d ? canon_lz(mul_lz(balanced(av), balanced(inv_i))) : aprime[i];
+            }
+        }
+    }
+    __syncthreads();
+    QI_TS(3);
+    // items: (row t, 4-entry group j), rows fastest (16 lanes = 16 rows of
+    // one group: the LDS pitch 4 x odd makes their b128 reads conflict-free)
+    const int KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
+    const int items = RB * nj * 16;
+    for (int it = tid; it < items; it += NT) {
+        const int tl = it & 15, jj = it >> 4;
+        const int t = 16 * (jj / nj) + tl, i0 = 4 * (jj % nj);
+        if (t >= L.R || i0 >= k)
+            continue;
+        uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
+        const uint4 c4 = *reinterpret_cast<const uint4*>(cinv + i0);
+        uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
+        const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+        for (int jb = 0; jb < 4; jb++)
+            e[jb] = i0 + jb < k ? canon_lz(mul_lz(static_cast<int32_t>(e[jb]), balanced(c[jb])))
+                                : 0u;
+        *reinterpret_cast<uint4*>(Mt + t * kp + i0) = uint4{e[0], e[1], e[2], e[3]};
+    }
+    __syncthreads();
+    QI_TS(4);
+    // per row: sum, scale test, the rare rescale (4 lanes per row, quad
+    // reductions by DPP; a row needs a unit scale with probability ~5 k /
+    // 65537, i.e. ~27 % of the stripes at k = 64, so the rescale runs on the
+    // quad too: s = 2, 3, ... as pack_row), kcorr / rscale / kmf
+    {
+        const int sub = tid & 3;
+        for (int t0 = 0; t0 < L.R; t0 += NT / 4) {
+            const int t = t0 + tid / 4;
+            uint32_t sum = 0, bad = 0;
+            if (t < L.R) {
+                for (int i0 = 4 * sub; i0 < k; i0 += 16) {
+                    const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
+                    sum += e4.x + e4.y + e4.z + e4.w;  // padding entries are 0
+                    bad |= coef_bad(e4.x) | coef_bad(e4.y) | coef_bad(e4.z) | coef_bad(e4.w);
+                }
+            }
+            bad |= __builtin_amdgcn_update_dpp(0u, bad, 0xB1, 0xf, 0xf, false);
+            bad |= __builtin_amdgcn_update_dpp(0u, bad, 0x4E, 0xf, 0xf, false);
+            int32_t rs = 1;
+            if (bad) {  // quad-uniform, rare
+                uint32_t* row = Mt + t * kp;
+                uint32_t sc = 0;
+                for (uint32_t cand = 2; cand < 256 && !sc; cand++) {
+                    // |s^-1| <= 32766 (the epilogue's v_mul_i32_i24)
+                    const uint32_t ci = inv_lz(cand);
+                    if (ci - 32767u < 4u)
+                        continue;
+                    uint32_t fail = 0;
+                    for (int i = sub; i < k; i += 4)
+                        fail |= coef_bad(canon_lz(static_cast<int32_t>(row[i] * cand)));
+                    fail |= __builtin_amdgcn_update_dpp(0u, fail, 0xB1, 0xf, 0xf, false);
+                    fail |= __builtin_amdgcn_update_dpp(0u, fail, 0x4E, 0xf, 0xf, false);
+                    if (!fail) {
+                        sc = cand;
+                        rs = balanced(ci);
+                    }
+                }
+                if (!sc)  // never seen (p ~ 2^-1000): mark the stripe undecodable
+                    atomicOr(err, kErrOorTruncated);
+                sum = 0;
+                for (int i = sub; i < k; i += 4) {
+                    row[i] = canon_lz(static_cast<int32_t>(row[i] * (sc ? sc : 1u)));
+                    sum += row[i];
+                }
+            }
+            sum += __builtin_amdgcn_update_dpp(0u, sum, 0xB1, 0xf, 0xf, false);
+            sum += __builtin_amdgcn_update_dpp(0u, sum, 0x4E, 0xf, 0xf, false);
+            if (t >= L.R || sub != 0)
+                continue;
+            // sum < 2^24: two folds, then canonical
+            const uint32_t sq = canon_lz(fold(static_cast<int32_t>(sum)));
+            mat[L.kcorr() + t] = static_cast<int32_t>(canon_lz(mul_lz(balanced(sq), 32768)));
+            mat[L.rscale() + t] = rs;
+            if (KS) {
+                mat[L.kmf() + t] = static_cast<int32_t>(canon_lz(mul_lz(balanced(sq), 32896)));
+                mat[L.rscale_mf() + t] = rs;
+            }
+        }
+    }
+    __syncthreads();
+    QI_TS(5);
+    // the operand tiles (pack_mf_dword's layout: [a | 0], [0 | b], [b | a];
+    // the zero halves are not written at KS >= 4, the kernel never reads
+    // them): items rows-fastest, so a wave's stores fill whole tile lines
+    int32_t* mf = mat + L.mf();
+    if (KS) {
+        for (int it = tid; it < items; it += NT) {
+            const int tl = it & 15, jj = it >> 4;
+            const int j = jj % nj, rb = jj / nj;
+            const int t = 16 * rb + tl, i0 = 4 * j;
+            uint32_t aw = 0, bw = 0;
+            if (t < L.R && i0 < k) {
+                const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
+                const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                for (int jb = 0; jb < 4; jb++) {
+                    if (i0 + jb < k) {
+                        int32_t a, b;
+                        split_i8(e[jb], a, b);
+                        aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
+                        bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
+                    }
+                }
+            }
+#pragma unroll
+            for (int half = 0; half < 2; half++) {
+                const int K = half * KH + i0;
+                const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
+                const size_t base =
+                    static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl) * 2 + dw;
+                if (KS < 4 || half == 0)
+                    mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
+                if (KS < 4 || half == 1)
+                    mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
+                mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
+            }
+        }
+    }
+    // the canonical `plain` rows and the dot2 kernel's packed pairs: items
+    // entries-fastest, so a wave's stores are contiguous runs (rows-fastest
+    // 16-byte pieces scattered over the rows had made the round-1 context
+    // store-bound)
+    int32_t* plain = mat + L.plain();
+    const int ng = (k + 3) / 4;
+    for (int it = tid; it < L.R * ng; it += NT) {
+        const int t = it / ng, i0 = 4 * (it - t * ng);
+        const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
+        const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+        for (int jb = 0; jb < 4; jb++)
+            if (i0 + jb < k)
+                plain[static_cast<size_t>(t) * k + i0 + jb] = static_cast<int32_t>(e[jb]);
+        int32_t* packed = mat + static_cast<size_t>(t) * L.KP;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int i = i0 + 2 * h;
+            if (i < k) {
+                const int32_t lo = balanced(e[2 * h]);
+                const int32_t hi = i + 1 < k ? balanced(e[2 * h + 1]) : 0;
+                packed[i >> 1] = static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xffffu) |
+                                                      (static_cast<uint32_t>(hi) << 16));
+            }
+        }
+    }
+    // packed pairs past kin up to KP stay zero (the dot2 kernel's padding)
+    const int pz = (k + 1) / 2, npz = L.KP - pz;
+    for (int it = tid; it < L.R * npz; it += NT)
+        mat[static_cast<size_t>(it / npz) * L.KP + pz + it % npz] = 0;
+    QI_TS(6);
+}
+
+int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
+                      const uint16_t* d_ids, int S, int32_t* d_ctx,
+                      long long ctx_stride, const Oor* in_oor, int slot_base,
+                      int by_pos, long long words, uint32_t* err, hipStream_t st)
+{
+    if (k > 256 || S <= 0)
+        return -3;
+    Oor none{nullptr, nullptr, 0, 0};
+    if (k > 128) {
+        // the matrix rows in the context itself (no LDS image); 1024 threads
+        // keep 4x more of the packing and tile passes' row loads in flight
+        // (k256 decode 0.81 -> 0.77 ms, k200 2.09 -> 2.05 ms)
+        hipLaunchKernelGGL((decode_ctx_kernel<1024, true>), dim3(S), dim3(1024), 0, st, k, r,
+                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
+                           slot_base, by_pos, words, err);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
+    RPow2 rp{};
+    uint32_t e = r;
+    for (int b = 0; b < 16; b++, e = mulmod_c(e, e))
+        rp.v[b] = balanced(e);
+    int lgn = 0;
+    while (lgn < 16 && (1u << lgn) < static_cast<uint32_t>(n))
+        lgn++;
+    const size_t lds = static_cast<size_t>(k) * ctx_pitch(k) * 4;
+    // k > 64: up to 68 KB (k = 128) of dynamic LDS, opted in
+    // per launch (cheap; the device may differ between calls)
+    if (lds > 65536 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_ctx_lds_kernel<256>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(lds)) != hipSuccess)
+        return -2;
+    // 2 waves at k <= 32: wave 1 routes the marks while wave 0 builds A(x)
+    if (k > 32)
+        hipLaunchKernelGGL((decode_ctx_lds_kernel<256>), dim3(S), dim3(256), lds, st, k, rp, lgn,
+                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
+                           slot_base, by_pos, words, err);
+    else
+        hipLaunchKernelGGL((decode_ctx_lds_kernel<128>), dim3(S), dim3(128), lds, st, k, rp, lgn,
+                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
+                           slot_base, by_pos, words, err);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace qi

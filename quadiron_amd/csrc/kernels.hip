@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <string>
 
 #include "fnt_codelets.h"
@@ -857,7 +858,8 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(MatArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// Matrix apply on the matrix cores (v_mfma_i32_16x16x32_i8), kin <= 64.
+// Matrix apply on the matrix cores (v_mfma_i32_16x16x32_i8 at KS = 1,
+// v_mfma_i32_16x16x64_i8 above), kin <= 256.
 //
 // The product of matrix_kernel, out[t] = sum_i M[t][i] x_i mod q, with the
 // u16 inputs and the row-scaled coefficients split into signed bytes:
@@ -868,8 +870,9 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(MatArgs a)
 //   D0 = sum a h',  D1 = sum b l',  D2 = sum b h' + a l'
 // -- three int8 GEMMs over K = [h' rows ; l' rows] against the per-stripe
 // operand tiles [a|0], [0|b], [b|a] (matrix_pack.h pack_mf_dword; D1 starts
-// at kmf[t] = 32896 sum c).  |D| < 2^21 for kin <= 64, so the int32
-// accumulators and the epilogue never overflow.  The dot2 kernel's ~19 VALU
+// at kmf[t] = 32896 sum c).  |D| <= 2 kin 128^2: up to kin = 128 (2^22)
+// 256 D2 + D1 - D0 stays inside int32; at KS = 16 (kin <= 256, |D2| <= 2^23)
+// the epilogue folds D2 before the shift.  The dot2 kernel's ~19 VALU
 // per (output, column) become ~5 of epilogue, so the decode is HBM-bound
 // rather than VALU-bound.
 //
@@ -1024,17 +1027,58 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     // this thread's CPL columns of every RG-th row, all row loads issued back
     // to back; rows past kin load a clamped row (their operand bytes are 0)
     uint32_t w[KH / RG][CPL / 2];
+    if constexpr (G::kTpr % 64 == 0) {
+        // the row group is wave-uniform: every id of the thread's rows in
+        // SGPRs first (the scalar loads issue together; loading each id
+        // next to its row load made a chain of KH dependent scalar loads,
+        // one lgkmcnt(0) per row), then the row loads back to back -- with
+        // one source region (every decode but the systematic one, and the
+        // encode) a row offset is one scalar multiply
+        int idv[KH / RG];
+        if (sid && !src.by_pos) {
 #pragma unroll
-    for (int r = 0; r < KH / RG; r++) {
-        const int i = r * RG + rg;
-        const int ii = i < kin ? i : kin - 1;
-        const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
-        const bool lo = id < src.split;
-        Region<true> g = g0;
-        g.r = lo ? g0.r : g1.r;
-        const uint32_t off = static_cast<uint32_t>(
-            lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
-        ld_dw<CPL / 2, true, kAuxLd>(g, off, voff, w[r]);
+            for (int r = 0; r < KH / RG; r++) {
+                const int i = r * RG + rg;
+                idv[r] = sid[i < kin ? i : kin - 1];
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < KH / RG; r++) {
+                const int i = r * RG + rg;
+                idv[r] = i < kin ? i : kin - 1;
+            }
+        }
+        if (!src.base1) {
+            const uint32_t rsb = static_cast<uint32_t>(src.rs0 * 2);
+#pragma unroll
+            for (int r = 0; r < KH / RG; r++)
+                ld_dw<CPL / 2, true, kAuxLd>(g0, static_cast<uint32_t>(idv[r]) * rsb, voff,
+                                             w[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < KH / RG; r++) {
+                const int id = idv[r];
+                const bool lo = id < src.split;
+                Region<true> g = g0;
+                g.r = lo ? g0.r : g1.r;
+                const uint32_t off = static_cast<uint32_t>(
+                    lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
+                ld_dw<CPL / 2, true, kAuxLd>(g, off, voff, w[r]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < KH / RG; r++) {
+            const int i = r * RG + rg;
+            const int ii = i < kin ? i : kin - 1;
+            const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
+            const bool lo = id < src.split;
+            Region<true> g = g0;
+            g.r = lo ? g0.r : g1.r;
+            const uint32_t off = static_cast<uint32_t>(
+                lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
+            ld_dw<CPL / 2, true, kAuxLd>(g, off, voff, w[r]);
+        }
     }
     const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) +
                           4 * ((cl % 64) / 16) + cl % 4;
@@ -1286,395 +1330,297 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// Per-stripe decode context: the Lagrange form of DecodeContext::init
-// (src/fec_context.h:232-274).  For received points x_i = r^{id_i}:
-//   A(x) = prod_j (x - x_j),  Q_i = A / (x - x_i),  A'(x_i) = Q_i(x_i)
-//   mode 0: M[t][i] = coef_t(Q_i) / A'(x_i)       (non-systematic)
-//   mode 1: M[t][i] = Q_i(r^t)   / A'(x_i)        (systematic)
-// plus the OOR route table of the stripe (decode_prepare's props walk,
-// src/fec_base.h:1361-1404, precomputed per tile).
-// One workgroup per stripe (64 lanes for k <= 32, else 256); k <= 256.
+// Pipelined persistent matrix-core kernel for short matrices (R <= 64 rows,
+// 16 < kin <= 64: the decodes of 17 <= k <= 64, e.g. BASELINE cfg3).
+//
+// The per-launch kernel above stages a 512-column tile (68 KB of image),
+// computes it, and exits: with two blocks per CU, every block's row loads
+// (and its preamble: ids, route table, operand tiles) sit on the critical
+// path.  Here a grid of (blocks per CU x CUs) blocks walks contiguous
+// ranges of 256-column tiles; while a tile is on the matrix cores, the
+// block's next tile is already in flight into registers (16 b64 row loads
+// per thread), and the operand tiles stay in registers while the stripe
+// does.  46 KB of LDS per block: 3 blocks (12 waves) per CU.
+// Per tile: wait for the rows -> barrier -> byte-plane image + marks ->
+// barrier -> issue the next tile's rows -> MFMAs, epilogue, stores.
+// Wave w takes row block w % nrb over super tiles [(w / nrb) nrb, +nrb)
+// (nrb = RB, 3 -> 4): every wave issues the same MFMA count.
 // ---------------------------------------------------------------------------
-// canonical a * b mod 65537 for a, b in [0, 65536]: with 2^16 = -1 and
-// 2^32 = 1, p = p0 + p1 2^16 + p2 2^32 reduces to p0 - p1 + p2
-__device__ __forceinline__ uint32_t mulm(uint32_t a, uint32_t b)
-{
-    // balanced operands (|a|, |b| <= 32768): the product fits int32 and one
-    // full-rate v_mul_i32_i24 forms it (the 64-bit product took two
-    // quarter-rate v_mul_{lo,hi}_u32 on the serial Lagrange chains)
-    const int32_t ab = static_cast<int32_t>(a) - (a > 32768u ? 65537 : 0);
-    const int32_t bb = static_cast<int32_t>(b) - (b > 32768u ? 65537 : 0);
-    const int32_t p = __mul24(ab, bb);                      // |p| <= 2^30
-    const int32_t v = (p & 0xffff) - (p >> 16);             // [-16384, 81919]
-    const int32_t w = v < 0 ? v + 65537 : v;                // [0, 81919]
-    return static_cast<uint32_t>(w >= 65537 ? w - 65537 : w);
-}
-__device__ __forceinline__ uint32_t addm(uint32_t a, uint32_t b)
-{
-    const uint32_t c = a + b;
-    return c >= 65537u ? c - 65537u : c;
-}
-__device__ __forceinline__ uint32_t subm(uint32_t a, uint32_t b)
-{
-    return a >= b ? a - b : a + 65537u - b;
-}
-__device__ __forceinline__ uint32_t powm(uint32_t b, uint32_t e)
-{
-    uint32_t r = 1;
-    for (; e; e >>= 1) {
-        if (e & 1)
-            r = mulm(r, b);
-        b = mulm(b, b);
-    }
-    return r;
-}
+template <int KS>
+struct PipeTile {
+    static constexpr int kThreads = 256;
+    static constexpr int kCols = 256;          // columns per tile
+    static constexpr int kRows = 16 * KS;      // rows per byte plane (KH)
+    static constexpr int kPitch = kCols + 16;  // LDS row pitch: +4 banks/row
+    static constexpr size_t kImg = static_cast<size_t>(2 * kRows) * kPitch;
+    static constexpr int kStagePitch = 144;
+    static constexpr size_t kStage = 16 * kStagePitch;
+    static constexpr size_t kMarks = kImg + 4 * kStage;
+    static constexpr size_t kLds = kMarks + 2 * 4 * kMaxTileOor + 16;
+    static constexpr int kRpt = kRows / 4;  // rows per thread (row group = wave)
+};
 
-// NT threads: the Lagrange part runs on the first wave (lane = point); the
-// row packing and the MFMA operand tiles use every thread (NT = 256 for
-// k > 32, where they dominate and there are few stripes per launch).
-// pack_row (matrix_pack.h) on a group of LPR adjacent lanes (a power of 2,
-// <= 16), lane `sub` taking entries sub, sub + LPR, ...: the column scale
-// 1 / A'(x_i) applied, the same row scale search (uniform in the group),
-// packed pairs, canonical `plain` entries, kcorr / rscale / kmf, and the
-// row-scaled entries written back to the LDS row for the tiles.  Entries
-// lane-fastest: a group's global stores are runs of LPR dwords (4 lanes per
-// row with 16-byte runs took 17 of the 43 us of a k = 64 context).
-__device__ __forceinline__ uint32_t grp_or(uint32_t v, int lpr)
+#ifndef QI_PIPE_WAVES
+#define QI_PIPE_WAVES 2
+#endif
+template <int KS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QI_PIPE_WAVES))) void
+matrix_pipe_kernel(MatArgs a, long long n_tiles, int tps)
 {
-    for (int m = 1; m < lpr; m <<= 1)
-        v |= __shfl_xor(v, m, lpr);
-    return v;
-}
-__device__ __forceinline__ uint32_t grp_add(uint32_t v, int lpr)
-{
-    for (int m = 1; m < lpr; m <<= 1)
-        v += __shfl_xor(v, m, lpr);
-    return v;
-}
-__device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLayout& L,
-                             int t, int32_t* block, int sub, int lpr)
-{
-    // the lane's entries i = sub + m lpr (m < 16: k <= 256 at lpr = 16) in
-    // registers: every row load is issued up front (rows in global memory
-    // for k > 128), and the packed pairs take the odd entry from the
-    // neighbour lane by shuffle instead of re-reading the row
-    constexpr int ME = 16;
-    const int kin = L.kin, KP = L.KP;
-    uint32_t v[ME];
-#pragma unroll
-    for (int m = 0; m < ME; m++) {
-        const int i = sub + m * lpr;
-        v[m] = i < kin ? row[i] : 0u;
-    }
-    uint32_t bad = 0;
-#pragma unroll
-    for (int m = 0; m < ME; m++) {
-        const int i = sub + m * lpr;
-        if (i < kin) {
-            v[m] = mulm(v[m], cscale[i]);
-            bad |= !coef_ok(balanced(v[m]));
-        }
-    }
-    bad = grp_or(bad, lpr);
-    uint32_t s = 1;
-    while (bad) {  // rare; s, si and bad are uniform in the group
-        s++;
-        const int32_t si = balanced(powm(s, 65535u));
-        if (iabs32(si) > 32766)
-            continue;
-        bad = 0;
-#pragma unroll
-        for (int m = 0; m < ME; m++) {
-            const int i = sub + m * lpr;
-            if (i < kin)
-                bad |= !coef_ok(balanced(mulm(v[m], s)));
-        }
-        bad = grp_or(bad, lpr);
-    }
-    int32_t* packed = block + static_cast<size_t>(t) * KP;
-    int32_t* plain = block + L.plain();
-    uint32_t sum = 0;  // <= 256 * 65536 = 2^24
-#pragma unroll
-    for (int m = 0; m < ME; m++) {
-        const int i = sub + m * lpr;
-        if (s != 1 && i < kin)
-            v[m] = mulm(v[m], s);
-        // pair (i, i + 1) for even i: the odd entry sits on lane sub + 1
-        const uint32_t odd = __shfl_xor(v[m], 1, lpr);
-        if (i < kin) {
-            row[i] = v[m];
-            plain[static_cast<size_t>(t) * kin + i] = static_cast<int32_t>(v[m]);
-            sum += v[m];
-            if (!(sub & 1)) {
-                const int32_t lo = balanced(v[m]);
-                const int32_t hi = i + 1 < kin ? balanced(odd) : 0;
-                packed[i >> 1] = static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xffffu) |
-                                                      (static_cast<uint32_t>(hi) << 16));
-            }
-        }
-    }
-    // pairs past kin up to KP stay zero (the dot2 kernel's padding)
-    for (int j = (kin + 1) / 2 + sub; j < KP; j += lpr)
-        packed[j] = 0;
-    sum = grp_add(sum, lpr);
-    if (sub == 0) {
-        // sum mod q by two folds (2^16 = -1), then canonical
-        int32_t f = static_cast<int32_t>(sum & 0xffffu) - static_cast<int32_t>(sum >> 16);
-        f = f < 0 ? f + 65537 : f;
-        const uint32_t sq = static_cast<uint32_t>(f >= 65537 ? f - 65537 : f);
-        block[L.kcorr() + t] = static_cast<int32_t>(mulm(sq, 32768u));
-        block[L.rscale() + t] = s == 1 ? 1 : balanced(powm(s, 65535u));
-        if (L.KS()) {
-            block[L.kmf() + t] = static_cast<int32_t>(mulm(sq, 32896u));
-            block[L.rscale_mf() + t] = block[L.rscale() + t];
-        }
-    }
-}
+    using G = PipeTile<KS>;
+    constexpr int KH = G::kRows, RSB = G::kPitch, RPT = G::kRpt;
+    extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
+    uint8_t* img = qi_lds;
+    int* s_i = reinterpret_cast<int*>(qi_lds + G::kMarks);
+    uint32_t* s_col = reinterpret_cast<uint32_t*>(s_i + kMaxTileOor);
+    int* s_cnt = reinterpret_cast<int*>(s_col + kMaxTileOor);
+    const MatLayout L = a.L;
+    const RowSrc src = a.src;
+    const RowDst dst = a.dst;
+    const MatExt ext = a.ext;
+    const Oor in_oor = a.in_oor;
+    const Oor out_oor = a.out_oor;
+    const int kin = L.kin;
+    const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+    const int g = l >> 4, q = (l & 15) >> 1, p = l & 1, tl = l & 15;
+    const int RB = L.RB();
+    const int nrb = RB == 3 ? 4 : RB;
+    const int rb = wv % nrb, st0 = (wv / nrb) * nrb;
+    const long long t_begin = static_cast<long long>(blockIdx.x) * n_tiles / gridDim.x;
+    const long long t_end = static_cast<long long>(blockIdx.x + 1) * n_tiles / gridDim.x;
+    if (t_begin >= t_end)
+        return;  // block-uniform
+    const bool rec = out_oor.counts != nullptr;
+    const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
+    const uint32_t rsb0 = static_cast<uint32_t>(src.rs0 * 2);
+    const uint32_t cl = static_cast<uint32_t>(l) * 4;  // staging columns of this lane
+    const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) + 4 * ((cl % 64) / 16) + cl % 4;
+    auto* lds = (__attribute__((address_space(3))) uint8_t*)img;
+    const uint32_t abase = static_cast<uint32_t>((8 * g + q) * RSB + 8 * p);
+    uint8_t* stg = qi_lds + G::kImg + wv * G::kStage;
 
-// LDS row pitch of the context kernel's k x k matrix: 4 x odd, >= k
-__host__ __device__ inline int ctx_pitch(int k)
-{
-    return (k + 3) / 8 * 8 + 4;
-}
-
-template <int NT, bool BIG>
-__global__ __launch_bounds__(NT) void decode_ctx_kernel(
-    int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
-    int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
-    int by_pos, long long words, uint32_t* err)
-{
-    __shared__ uint32_t xs[256];
-    __shared__ uint32_t A[257];
-    __shared__ uint32_t cinv[256];    // 1 / A'(x_i)
-    __shared__ uint32_t aprime[256];  // A'(x_i)
-    // k x k matrix, sized by the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
-    // limited the kernel to 4 workgroups per CU
-    extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
-    // row pitch = 4 x odd (>= k, a multiple of 4 words): the tile pass
-    // reads 16 rows x 16 bytes per wave (ds_read_b128) conflict-free (the
-    // odd pitch k | 1 had SQ_LDS_BANK_CONFLICT at 7.4 cycles per LDS
-    // instruction at k = 64)
-    const int s = blockIdx.x;
-    const int tid = threadIdx.x;
-    int32_t* mat = ctx + s * ctx_stride;
-    // BIG (128 < k <= 256): the k x k matrix (up to 256 KB) does not fit
-    // LDS; its rows live in the context's own `plain` section (pitch k),
-    // which the packing pass rewrites in place with the row-scaled entries
-    const int kp = BIG ? k : ctx_pitch(k);
-    uint32_t* Mt = BIG ? reinterpret_cast<uint32_t*>(mat + L.plain()) : qi_ctx_lds;
-    int32_t* cids = mat + L.words();
-    uint32_t* route = reinterpret_cast<uint32_t*>(cids + 2 * L.KP);
-    for (int i = k + tid; i < 2 * L.KP; i += NT)
-        cids[i] = 0;
-    const long long ntiles = route_tiles(words);
-
-    // route table: clear, then (after the barrier below) fill; the
-    // slow-tile list behind it starts empty
-    for (long long t = tid; t < ntiles; t += NT)
-        route[t * kRouteStride] = 0;
-    if (tid == 0)
-        route[ntiles * kRouteStride] = 0;
-    if (tid < k) {
-        const uint32_t id = ids[static_cast<long long>(s) * k + tid];
-        xs[tid] = powm(r, id);
-        cids[tid] = static_cast<int32_t>(id);
-    }
-    __syncthreads();
-    if (in_oor.counts && tid < k) {
-        const int id = ids[static_cast<long long>(s) * k + tid];
-        const int slot = (by_pos ? tid : id) - slot_base;
-        if (slot >= 0) {
-            const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
-            uint32_t c = in_oor.counts[bk];
-            if (c > static_cast<uint32_t>(in_oor.cap)) {
-                atomicOr(err, kErrOorTruncated);
-                c = static_cast<uint32_t>(in_oor.cap);
-            }
-            for (uint32_t e = 0; e < c; e++) {
-                const uint32_t w = in_oor.entries[bk * in_oor.cap + e];
-                if (w >= words)
-                    continue;
-                uint32_t* rt = route + (w / kRouteTile) * kRouteStride;
-                const uint32_t p = atomicAdd(rt, 1u);
-                if (p < static_cast<uint32_t>(kRouteCap))
-                    rt[1 + p] = (static_cast<uint32_t>(tid) << 16) | (w % kRouteTile);
-            }
-        }
-    }
-    // A(x) = prod_i (x - x_i), lane d holding coefficient d (and d + 64,
-    // d + 128, ... for k > 64).  A is monic: A[k] = 1 is set explicitly, so
-    // k = 64 (128, 256) needs no 65th (129th, 257th) coefficient slot.
-    if (tid < 64) {  // wave 0 (wave-uniform)
-        uint32_t a = tid == 0 ? 1u : 0u;
-        if (k <= 64) {
-            for (int i = 0; i < k; i++) {
-                uint32_t prev = __shfl_up(a, 1);
-                if (tid == 0)
-                    prev = 0;
-                a = subm(prev, mulm(xs[i], a));
+    // rows of tile t: this thread's 4 columns of rows wv, wv + 4, ...
+    uint32_t w[RPT][2];
+    auto issue_rows = [&](long long t) {
+        const int s = static_cast<int>(t / tps);
+        const long long col0 = (t - static_cast<long long>(s) * tps) * G::kCols;
+        const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
+        int idv[RPT];
+        if (sid && !src.by_pos) {
+#pragma unroll
+            for (int r = 0; r < RPT; r++) {
+                const int i = 4 * r + wv;
+                idv[r] = sid[i < kin ? i : kin - 1];
             }
         } else {
-            // slot u holds coefficient 64 u + lane (u < nslot <= 4)
-            const int nslot = (k + 63) / 64;
-            uint32_t au[4] = {a, 0u, 0u, 0u};
-            for (int i = 0; i < k; i++) {
-                uint32_t prev[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++)
-                    prev[u] = __shfl_up(au[u], 1);
-#pragma unroll
-                for (int u = 1; u < 4; u++) {
-                    const uint32_t top = __shfl(au[u - 1], 63);  // 64 u - 1 -> 64 u
-                    if (tid == 0)
-                        prev[u] = top;
-                }
-                if (tid == 0)
-                    prev[0] = 0;
-                const uint32_t x = xs[i];
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (u < nslot)
-                        au[u] = subm(prev[u], mulm(x, au[u]));
-            }
-            a = au[0];
-#pragma unroll
-            for (int u = 1; u < 4; u++)
-                if (u < nslot)
-                    A[64 * u + tid] = au[u];
-        }
-        A[tid] = a;
-        if (tid == 0)
-            A[k] = 1;
-    }
-    __syncthreads();
-    if (tid < k) {
-        // Q_i = A / (x - x_i) by synthetic division from the top, and
-        // A'(x_i) = Q_i(x_i) by Horner over the same coefficients (two
-        // interleaved chains; the product prod_{j != i} (x_i - x_j) was a
-        // third serial chain).  The rows hold the unscaled values; the
-        // column scale 1 / A'(x_i) is applied by the packing pass.
-        const uint32_t xi = xs[tid];
-        uint32_t q = 1, h = 1;  // A[k]; Q_i(x_i) so far
-        if (mode == 0)
-            Mt[(k - 1) * kp + tid] = 1;
-        for (int j = k - 1; j >= 1; j--) {
-            q = addm(A[j], mulm(xi, q));
-            if (mode == 0)
-                Mt[(j - 1) * kp + tid] = q;
-            h = addm(mulm(h, xi), q);
-        }
-        aprime[tid] = h;
-        cinv[tid] = powm(h, 65535u);
-    }
-    if (mode != 0) {
-        // systematic: M[t][i] = Q_i(r^t) / A'(x_i), one thread per row t,
-        // with Q_i(r^t) = A(r^t) / (r^t - x_i): 0 when r^t is another
-        // received point (A(r^t) = 0), A'(x_i) when it is x_i itself.  The
-        // k inverses of a row come from one inversion (prefix products, the
-        // running inverse walked back), so a row costs ~3k + 24 serial
-        // multiplies (Horner of every Q_i at every r^t took k^2 per lane).
-        __syncthreads();
-        if (tid < k) {
-            uint32_t* row = Mt + tid * kp;
-            const uint32_t et = powm(r, static_cast<uint32_t>(tid));
-            uint32_t av = 1;  // A(r^t), A monic
-            for (int j = k - 1; j >= 0; j--)
-                av = addm(mulm(av, et), A[j]);
-            uint32_t pre = 1;
-            for (int i = 0; i < k; i++) {
-                const uint32_t d = subm(et, xs[i]);
-                row[i] = pre;
-                pre = mulm(pre, d ? d : 1u);
-            }
-            uint32_t inv = powm(pre, 65535u);
-            for (int i = k - 1; i >= 0; i--) {
-                const uint32_t d = subm(et, xs[i]);
-                const uint32_t inv_i = mulm(inv, row[i]);
-                inv = mulm(inv, d ? d : 1u);
-                row[i] = d ? mulm(av, inv_i) : aprime[i];
+            for (int r = 0; r < RPT; r++) {
+                const int i = 4 * r + wv;
+                idv[r] = i < kin ? i : kin - 1;
             }
         }
-    }
-    __syncthreads();
-    {
-        // LPR lanes per row: 4 entries per lane at k = 64
-        const int q4 = (k + 3) / 4;
-        const int lpr = q4 <= 4 ? 4 : q4 <= 8 ? 8 : 16;
-        for (int t = tid / lpr; t < L.R; t += NT / lpr)
-            pack_row_grp(Mt + t * kp, cinv, L, t, mat, tid & (lpr - 1), lpr);
-    }
-    if (L.KS()) {
-        // the matrix-core operand tiles, from the row-scaled entries in LDS
-        __syncthreads();
-        // per (row t, 4 consecutive entries): split once, then place the
-        // a / b byte words in their tile dwords (pack_mf_dword's layout;
-        // rows t >= R are zero).  Items run row-fastest, so 16 lanes read
-        // 16 rows' entries i0..i0+3 (one ds_read_b128 each) and a wave's
-        // stores cover whole 128-byte tile lines (16 rows x 2 dwords).  At
-        // KS >= 4 the zero halves of [a | 0] and [0 | b] are not written:
-        // matrix_mfma_kernel skips those K-steps (and never loads them).
-        const int KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
-        int32_t* mf = mat + L.mf();
-        // BIG: the rows come from global memory; 4 items per thread have
-        // their loads in flight together (the stores to the tiles may alias
-        // the rows as far as the compiler knows, so it would not overlap
-        // the iterations itself)
-        constexpr int IB = BIG ? 4 : 1;
-        const int items = RB * nj * 16;
-        for (int it0 = tid; it0 < items; it0 += IB * NT) {
-            uint32_t e[IB][4];
+        const uint32_t voff = static_cast<uint32_t>((col0 + cl) * 2);
+        const Region<true> g0(src.base0 + s * src.ss0, ext.e0);
+        if (!src.base1) {
 #pragma unroll
-            for (int ib = 0; ib < IB; ib++) {
-                const int it = it0 + ib * NT;
-                const int tl4 = it & 15, jj = it >> 4;
-                const int t = 16 * (jj / nj) + tl4, i0 = 4 * (jj % nj);
-                const bool live = it < items && t < L.R && i0 < k;
-                if constexpr (BIG) {  // global rows, pitch k: no 16-byte alignment
+            for (int r = 0; r < RPT; r++)
+                ld_dw<2, true, kAuxLd>(g0, static_cast<uint32_t>(idv[r]) * rsb0, voff, w[r]);
+        } else {
+            const Region<true> g1(src.base1 + s * src.ss1, ext.e1);
 #pragma unroll
-                    for (int jb = 0; jb < 4; jb++)
-                        e[ib][jb] = live && i0 + jb < k ? Mt[t * kp + i0 + jb] : 0u;
-                } else if (live) {
-                    const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
-                    e[ib][0] = e4.x;
-                    e[ib][1] = e4.y;
-                    e[ib][2] = e4.z;
-                    e[ib][3] = e4.w;
-                }
+            for (int r = 0; r < RPT; r++) {
+                const int id = idv[r];
+                const bool lo = id < src.split;
+                Region<true> gg = g0;
+                gg.r = lo ? g0.r : g1.r;
+                const uint32_t off = static_cast<uint32_t>(
+                    lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
+                ld_dw<2, true, kAuxLd>(gg, off, voff, w[r]);
             }
+        }
+    };
+
+    // the stripe's operand tiles of row block rb, kmf / row scale / output
+    // rows of this lane (reloaded when the stripe changes)
+    qi_v2i bop[KS][3];
+    int32_t kt = 0, rs = 1, pr[3] = {0, 0, 0};
+    int cur = -1;
+    auto load_ops = [&](int s) {
+        const int32_t* M = a.mat + s * a.ms;
+        const int32_t* mf = M + L.mf();
 #pragma unroll
-            for (int ib = 0; ib < IB; ib++) {
-                const int it = it0 + ib * NT;
-                if (it >= items)
-                    break;
-                const int tl4 = it & 15, jj = it >> 4;
-                const int j = jj % nj, rb = jj / nj;
-                const int t = 16 * rb + tl4, i0 = 4 * j;
-                uint32_t aw = 0, bw = 0;
-                if (t < L.R && i0 < k) {
+        for (int ks = 0; ks < KS; ks++)
 #pragma unroll
-                    for (int jb = 0; jb < 4; jb++) {
-                        if (i0 + jb < k) {
-                            int32_t a, b;
-                            split_i8(e[ib][jb], a, b);
-                            aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
-                            bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
-                        }
+            for (int ty = 0; ty < 3; ty++)
+                bop[ks][ty] = *reinterpret_cast<const qi_v2i*>(
+                    mf + ((rb * KS + ks) * 3 + ty) * 128 + l * 2);
+        const int t = 16 * rb + tl, tc = t < L.R ? t : L.R - 1;
+        const int32_t k0 = M[L.kmf() + tc], r0 = M[L.rscale_mf() + tc];
+        kt = t < L.R ? k0 : 0;
+        rs = t < L.R ? r0 : 1;
+        pr[0] = a.rowmap[tc];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int ot = 16 * rb + 8 * h + (l >> 3);
+            pr[1 + h] = a.rowmap[ot < L.R ? ot : L.R - 1];
+        }
+    };
+
+    issue_rows(t_begin);
+    for (long long t = t_begin; t < t_end; t++) {
+        const int s = static_cast<int>(t / tps);
+        const long long col0 = (t - static_cast<long long>(s) * tps) * G::kCols;
+        if (s != cur) {  // block-uniform
+            load_ops(s);
+            cur = s;
+        }
+        const int32_t* M = a.mat + s * a.ms;
+        const int32_t* plain = M + L.plain();
+        // marks of the received rows in this tile: the route table, or a
+        // bucket scan when it overflowed (or is absent)
+        int n_rm = 0;
+        const uint32_t* rm = nullptr;
+        bool scan = in_oor.counts != nullptr;
+        if (a.route && scan) {
+            const uint32_t* rt = a.route + s * a.rstride + (col0 / kRouteTile) * kRouteStride;
+            const uint32_t rc = rt[0];
+            if (rc <= static_cast<uint32_t>(kRouteCap)) {
+                n_rm = static_cast<int>(rc);
+                rm = rt + 1;
+                scan = false;
+            }
+        }
+        __syncthreads();  // the previous tile's image, marks and staging are free
+#pragma unroll
+        for (int r = 0; r < RPT; r++) {
+            const int i = 4 * r + wv;
+            const uint32_t hi = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x07050301u) ^ 0x80808080u;
+            const uint32_t lo = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x06040200u) ^ 0x80808080u;
+            *reinterpret_cast<uint32_t*>(img + i * RSB + lpos) = hi;
+            *reinterpret_cast<uint32_t*>(img + (KH + i) * RSB + lpos) = lo;
+        }
+        int n_lm = 0;
+        bool slow = false;
+        if (scan) {  // block-uniform; its barriers also publish the image
+            const OorScan sc{in_oor, a.ids ? a.ids + s * a.is : nullptr, src.by_pos,
+                             a.slot_base, kin, s, false};
+            const int cnt = scan_tile_marks(sc, col0, col0 + G::kCols, a.words, s_cnt, s_i,
+                                            s_col, a.err);
+            slow = cnt > kMaxTileOor;
+            n_lm = min(cnt, kMaxTileOor);
+        } else {
+            stage_route_marks(rm, n_rm, col0, s_i, s_col);
+            __syncthreads();
+            n_lm = n_rm;
+        }
+        // the next tile's rows fly while this one is on the matrix cores
+        if (t + 1 < t_end)
+            issue_rows(t + 1);
+
+        const int trow = 16 * rb + tl;
+        const bool live = trow < L.R;
+        const int tcl = live ? trow : L.R - 1;
+        const Region<true> go(dst.base + s * dst.ss, ext.eo);
+#pragma unroll 1
+        for (int st = st0; st < st0 + nrb; st++) {
+            qi_v4i acc[4][3];
+#pragma unroll
+            for (int T = 0; T < 4; T++) {
+                acc[T][0] = qi_v4i{0, 0, 0, 0};
+                acc[T][1] = qi_v4i{kt, kt, kt, kt};
+                acc[T][2] = qi_v4i{0, 0, 0, 0};
+                auto rd_a = [&](int ks) {
+                    auto* pa = (__attribute__((address_space(3))) qi_v2i*)(
+                        lds + abase + 32 * ks * RSB + (4 * st + T) * 16);
+                    return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
+                };
+#pragma unroll
+                for (int ks = 0; ks < KS; ks += 2) {
+                    const qi_v2i a0 = rd_a(ks), a1 = rd_a(ks + 1);
+                    const qi_v4i av{a0.x, a0.y, a1.x, a1.y};
+#pragma unroll
+                    for (int ty = 0; ty < 3; ty++) {
+                        if ((ty == 0 && ks >= KS / 2) || (ty == 1 && ks + 1 < KS / 2))
+                            continue;
+                        const qi_v4i b{bop[ks][ty].x, bop[ks][ty].y, bop[ks + 1][ty].x,
+                                       bop[ks + 1][ty].y};
+                        acc[T][ty] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, b, acc[T][ty],
+                                                                           0, 0, 0);
                     }
                 }
+            }
+            // epilogue: lane (g, t) holds row t, columns cb .. cb + 15
+            const long long cb = col0 + 64 * st + 16 * g;
+            int32_t y[16];
 #pragma unroll
-                for (int half = 0; half < 2; half++) {
-                    const int K = half * KH + i0;
-                    const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
-                    const size_t base =
-                        static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl4) * 2 + dw;
-                    if (KS < 4 || half == 0)
-                        mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
-                    if (KS < 4 || half == 1)
-                        mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
-                    mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
+            for (int T = 0; T < 4; T++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    y[4 * T + j] = fold(fold((acc[T][2][j] << 8) + acc[T][1][j] - acc[T][0][j]));
+            // restored OOR symbols (decode_prepare): see matrix_mfma_kernel
+            const uint32_t stc = static_cast<uint32_t>(col0 + 64 * st);
+            for (int e = 0; e < n_lm; e++) {
+                const uint32_t wcu = __builtin_amdgcn_readfirstlane(s_col[e]);
+                if (wcu - stc >= 64u)
+                    continue;
+                const int pos = __builtin_amdgcn_readfirstlane(s_i[e]);
+                const long long d = static_cast<long long>(wcu) - cb;
+                const int32_t corr = plain[tcl * kin + pos];
+#pragma unroll
+                for (int c = 0; c < 16; c++) {
+                    const int32_t yc = fold(fold(y[c] - corr));
+                    y[c] = (live && d == c) ? yc : y[c];
                 }
             }
+            if (__builtin_amdgcn_ballot_w64(rs != 1)) {
+#pragma unroll
+                for (int c = 0; c < 16; c++)
+                    y[c] = fold(fold(mul_i24_s(y[c], rs)));
+            }
+            uint32_t bad = 0;
+#pragma unroll
+            for (int c = 0; c < 16; c++)
+                bad |= static_cast<uint32_t>(y[c]);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64((bad >> 16) != 0) != 0, 0)) {
+#pragma unroll
+                for (int c = 0; c < 16; c++) {
+                    if (static_cast<uint32_t>(y[c]) > 65535u) {
+                        if (rec && live)
+                            record_oor(out_oor, s, pr[0], cb + c);
+                        y[c] = 0;
+                    }
+                }
+            }
+            qi_v4u o0, o1;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                o0[c] = pack_lo(static_cast<uint32_t>(y[2 * c]), static_cast<uint32_t>(y[2 * c + 1]));
+                o1[c] = pack_lo(static_cast<uint32_t>(y[8 + 2 * c]),
+                                static_cast<uint32_t>(y[8 + 2 * c + 1]));
+            }
+            // transpose through the wave's staging tile: whole 128-byte lines
+            *reinterpret_cast<qi_v4u*>(stg + tl * G::kStagePitch + 32 * g) = o0;
+            *reinterpret_cast<qi_v4u*>(stg + tl * G::kStagePitch + 32 * g + 16) = o1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int orow = 8 * h + (l >> 3), c = l & 7;
+                const qi_v4u v =
+                    *reinterpret_cast<const qi_v4u*>(stg + orow * G::kStagePitch + 16 * c);
+                const int ot = 16 * rb + orow;
+                const uint32_t vo =
+                    ot < L.R ? static_cast<uint32_t>(pr[1 + h]) * ors +
+                                   static_cast<uint32_t>((col0 + 64 * st + 8 * c) * 2)
+                             : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo), 0, kAuxStMf);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
+        if (slow && tid == 0)  // rare: see matrix_redo_kernel
+            push_slow_tile(a.slow, s, col0, G::kCols);
     }
 }
 
@@ -1869,6 +1815,21 @@ static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 //    4 waves per SIMD instead of 2) measured slower on the 1024 x 64 cfg3
 //    generator (1.37 vs 1.22 ms, gpurun_out r2f), so the block stays at 4
 //    waves.
+// A/B knob (temporary): QI_MATK=0 the per-launch kernel at 512 columns,
+// 1 the pipelined kernel, 2 the per-launch kernel at 256 columns
+static int matk_mode()
+{
+    static const int m = [] {
+        const char* e = std::getenv("QI_MATK");
+        return e ? e[0] - '0' : 0;
+    }();
+    return m;
+}
+static bool pipe_enabled()
+{
+    return matk_mode() == 1;
+}
+
 template <int KS>
 static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t st)
 {
@@ -1888,10 +1849,49 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
         (void)RB;
         return mfma_launch<KS, 4, 4, true>(a, wfull, S, st);
     } else {
+        if constexpr (KS == 2 || KS == 4) {
+            if (matk_mode() == 2) {
+                if (RB >= 4)
+                    return mfma_launch<KS, 4, 4, true>(a, wfull, S, st);
+                return mfma_launch<KS, 4, 4, false>(a, wfull, S, st);
+            }
+        }
         if (RB >= 4)
             return mfma_launch<KS, NSTS, 4, true>(a, wfull, S, st);
         return mfma_launch<KS, NSTS, 4, false>(a, wfull, S, st);
     }
+}
+
+// grid of the pipelined kernel: as many blocks as fit the chip at once
+template <int KS>
+static int pipe_launch(MatArgs a, long long wfull, int S, hipStream_t st)
+{
+    using G = PipeTile<KS>;
+    static std::atomic<int> grid_cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev >= 64)
+        return -2;
+    int grid = grid_cache[dev].load(std::memory_order_relaxed);
+    if (grid == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, reinterpret_cast<const void*>(&matrix_pipe_kernel<KS>), G::kThreads,
+                G::kLds) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                hipSuccess)
+            return -2;
+        grid = (per_cu > 0 ? per_cu : 1) * cus;
+        grid_cache[dev].store(grid, std::memory_order_relaxed);
+    }
+    const int tps = static_cast<int>(wfull / G::kCols);
+    const long long n_tiles = static_cast<long long>(tps) * S;
+    if (tps <= 0)
+        return -1;
+    a.tiles = tps;
+    const long long blocks = n_tiles < grid ? n_tiles : grid;
+    hipLaunchKernelGGL((matrix_pipe_kernel<KS>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(G::kThreads), G::kLds, st, a, n_tiles, tps);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
@@ -1918,6 +1918,10 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
         int rc;
         if (L.KS() == 1)
             rc = mfma_dispatch<1>(a, wfull, S, st);
+        else if (L.KS() == 2 && L.RB() <= 4 && pipe_enabled())
+            rc = pipe_launch<2>(a, wfull, S, st);
+        else if (L.KS() == 4 && L.RB() <= 4 && pipe_enabled())
+            rc = pipe_launch<4>(a, wfull, S, st);
         else if (L.KS() == 2)
             rc = mfma_dispatch<2>(a, wfull, S, st);
         else if (L.KS() == 4)
@@ -2005,42 +2009,6 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
     // tiles with more marks than the kernels' LDS list: see push_slow_tile
     const int grid = S < 1024 ? S : 1024;
     hipLaunchKernelGGL(matrix_redo_kernel, dim3(grid), dim3(kBlock), 0, st, a, S);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
-                      const uint16_t* d_ids, int S, int32_t* d_ctx,
-                      long long ctx_stride, const Oor* in_oor, int slot_base,
-                      int by_pos, long long words, uint32_t* err, hipStream_t st)
-{
-    if (k > 256 || S <= 0)
-        return -3;
-    Oor none{nullptr, nullptr, 0, 0};
-    if (k > 128) {
-        // the matrix rows in the context itself (no LDS image); 1024 threads
-        // keep 4x more of the packing and tile passes' row loads in flight
-        // (k256 decode 0.81 -> 0.77 ms, k200 2.09 -> 2.05 ms)
-        hipLaunchKernelGGL((decode_ctx_kernel<1024, true>), dim3(S), dim3(1024), 0, st, k, r,
-                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                           slot_base, by_pos, words, err);
-        return hipGetLastError() == hipSuccess ? 0 : -2;
-    }
-    const size_t lds = static_cast<size_t>(k) * ctx_pitch(k) * 4;
-    // k > 64: up to 68 KB (k = 128) of dynamic LDS, opted in
-    // per launch (cheap; the device may differ between calls)
-    if (lds > 65536 &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_ctx_kernel<256, false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(lds)) != hipSuccess)
-        return -2;
-    if (k > 32)
-        hipLaunchKernelGGL((decode_ctx_kernel<256, false>), dim3(S), dim3(256), lds, st, k, r,
-                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                           slot_base, by_pos, words, err);
-    else
-        hipLaunchKernelGGL((decode_ctx_kernel<64, false>), dim3(S), dim3(64), lds, st, k, r,
-                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                           slot_base, by_pos, words, err);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -1,8 +1,8 @@
-// General-k RS-FNT path (k > 64): NTT-structured encode and decode.
+// General-k RS-FNT path (k > 256): NTT-structured encode and decode.
 //
-// Codes with k > 64 do not fit the register codelets of encode_fnt_kernel
+// Codes with k > 256 do not fit the register codelets of encode_fnt_kernel
 // (K = ceil2(k) <= 64) nor the k x k interpolation matrices of the matrix
-// kernels, and their O(k^2) per column would lose to the transforms anyway.
+// kernels (k <= 256, whose byte-split products stay exact up to there).
 // They run the reference's own algorithm as column-batched NTTs:
 //
 //   non-systematic encode  NTT_n of the k data rows zero-padded to n

@@ -235,6 +235,7 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
             id[i] = i;
         ok = ok && hipMalloc(&p->d_rowid, id.size() * 4) == hipSuccess &&
              hipMemcpy(p->d_rowid, id.data(), id.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+
     }
     if (!ok) {
         qi_plan_destroy(p);

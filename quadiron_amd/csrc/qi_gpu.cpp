@@ -62,7 +62,7 @@ int build_ctx(qi_plan* p, const uint16_t* d_ids, int n_stripes, const Oor* in,
     if (p->ntt)
         return ntt_build_ctx(p, d_ids, n_stripes, static_cast<int32_t*>(d_ctx), cs, s);
     const MatLayout L = ctx_layout(p);
-    return launch_decode_ctx(p->k, p->r, p->sys ? 1 : 0, L, d_ids, n_stripes,
+    return launch_decode_ctx(p->k, p->n, p->r, p->sys ? 1 : 0, L, d_ids, n_stripes,
                              static_cast<int32_t*>(d_ctx), cs, in, slot_base, by_pos,
                              words, p->d_err, s);
 }

@@ -115,7 +115,8 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long mat_stride,
 //   kRouteStride u32) built from in_oor, then the slow-tile list
 //   (slow_words(words) u32, count cleared)
 //   (slot = by_pos ? position : id - slot_base); in_oor may be null.
-int launch_decode_ctx(int k, uint32_t r, int mode, const MatLayout& L,
+//   n: the code length (ids < n), r its root of unity
+int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
                       const uint16_t* d_ids, int n_stripes, int32_t* d_ctx,
                       long long ctx_stride, const Oor* in_oor, int slot_base,
                       int by_pos, long long words, uint32_t* d_err,

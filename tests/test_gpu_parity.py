@@ -356,6 +356,20 @@ def test_cfg4_all_patterns_distinct():
                      check_oracle=False)
 
 
+@pytest.mark.parametrize("k,m,S,P", [
+    (16, 48, 4096, 256),    # ~0.1 % of the stripes need a row scale
+    (64, 960, 96, 1024),    # ~27 %
+    (100, 28, 48, 1024),    # KS = 8
+    (128, 128, 24, 1024),
+])
+def test_decode_row_scales_many_stripes(k, m, S, P):
+    """Many random erasure patterns: the decode contexts whose interpolation
+    rows hold an entry neither kernel can take (balanced |c| > 32766 or
+    32640) are rescaled by a unit s on the GPU (pack_row's search); every
+    stripe must still decode back to its data."""
+    _batch_roundtrip(k, m, 0, S, P, seed=3 * k + S, n_craft=0, check_oracle=False)
+
+
 def test_empty_and_tiny_blocks(hip_lib):
     for B in (0, 1, 2, 3, 130):
         k, m = 3, 2

@@ -1,5 +1,5 @@
 """CPU: the compiler's resource report of the gfx950 kernels
-(build/obj/kernels.res, written by quadiron_amd/csrc/Makefile).  A hot kernel
+(build/obj/{kernels,ctx,ntt}.res, written by quadiron_amd/csrc/Makefile).  A hot kernel
 that spills to scratch memory runs through memory instead of registers (a
 y[16] epilogue array once landed there and doubled the decode time), so
 scratch use is an error outside the listed rare paths."""
@@ -9,7 +9,8 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RES = [os.path.join(ROOT, "build", "obj", f) for f in ("kernels.res", "ntt.res")]
+RES = [os.path.join(ROOT, "build", "obj", f)
+       for f in ("kernels.res", "ctx.res", "ntt.res")]
 
 # kernels allowed to use scratch: the adversarial-OOR recompute and the
 # K = 64 encode codelet (256 VGPRs at 2 waves/SIMD, 3-4 spilled registers;
