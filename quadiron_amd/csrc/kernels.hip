@@ -1815,8 +1815,9 @@ static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 //    4 waves per SIMD instead of 2) measured slower on the 1024 x 64 cfg3
 //    generator (1.37 vs 1.22 ms, gpurun_out r2f), so the block stays at 4
 //    waves.
-// A/B knob (temporary): QI_MATK=0 the per-launch kernel at 512 columns,
-// 1 the pipelined kernel, 2 the per-launch kernel at 256 columns
+// A/B knob (temporary): QI_MATK=1 runs the pipelined kernel instead of the
+// per-launch one (cfg3 decode 0.206 vs 0.179 ms, gpurun_out r3m2; 256-column
+// blocks of the per-launch kernel: 0.186 ms, encode 1.21 vs 1.07 ms)
 static int matk_mode()
 {
     static const int m = [] {
@@ -1849,13 +1850,6 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
         (void)RB;
         return mfma_launch<KS, 4, 4, true>(a, wfull, S, st);
     } else {
-        if constexpr (KS == 2 || KS == 4) {
-            if (matk_mode() == 2) {
-                if (RB >= 4)
-                    return mfma_launch<KS, 4, 4, true>(a, wfull, S, st);
-                return mfma_launch<KS, 4, 4, false>(a, wfull, S, st);
-            }
-        }
         if (RB >= 4)
             return mfma_launch<KS, NSTS, 4, true>(a, wfull, S, st);
         return mfma_launch<KS, NSTS, 4, false>(a, wfull, S, st);
