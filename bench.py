@@ -51,6 +51,8 @@ CONFIGS = {
     "k200": (200, 56, 65536, 64),    # n = 256
     "k256": (256, 768, 4096, 256),   # n = 1024
     "k300": (300, 212, 65536, 32),   # n = 512, len_2k = 1024 (NTT engine)
+    # cfg3's code at 64 KiB packets (the same bytes per step as cfg3)
+    "cfg3p64": (64, 960, 65536, 64),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 

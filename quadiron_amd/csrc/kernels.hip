@@ -58,6 +58,16 @@ static_assert(fold_rng(join(mul_rng(Rng{0, 65535}, 32768),
                                 mul_rng(Rng{0, 65535}, -32768))).hi == kTwHi,
               "twist output range");
 
+// x * c for a T-range x and a balanced row scale |c| <= 32766 as ONE
+// v_mul_i32_i24 (written out: the compiler cannot see that the lazily
+// reduced x fits 24 bits and emitted the quarter-rate v_mul_lo_u32)
+__device__ __forceinline__ int32_t mul_rs(int32_t x, int32_t c)
+{
+    int32_t r;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(x), "v"(c));
+    return r;
+}
+
 // pack the low halves of two dwords: [a.lo, b.lo] (one v_perm_b32)
 __device__ __forceinline__ uint32_t pack_lo(uint32_t a, uint32_t b)
 {
@@ -724,7 +734,7 @@ __device__ __forceinline__ void matrix_compute(
         if (rs != 1) {
 #pragma unroll
             for (int c = 0; c < COLS; c++)
-                y[c] = fold(fold(mul_i24_s(y[c], rs)));
+                y[c] = fold(fold(mul_rs(y[c], rs)));
         }
         uint32_t o[COLS];
         uint32_t bad = 0;
@@ -913,6 +923,8 @@ struct MfmaTile {
     static constexpr size_t kLdsStaged = kLds + NW * kStage;
     // staging loads: CPL columns per lane (b64 or b32), TPR lanes per image
     // row, RG row groups
+    // (b64 staging loads at 512-column blocks -- 32 rows per thread
+    // instead of 64 -- measured the cfg3 encode 6 % slower, decode equal)
     static constexpr int kCpl = kCols >= 4 * kThreads ? 4 : 2;
     static constexpr int kTpr = kCols / kCpl;
     static constexpr int kRg = kThreads / kTpr;
@@ -1022,6 +1034,13 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     const int rb0 = rsplit ? wv : 0, rbs = rsplit ? NW : 1;
     constexpr int nst = rsplit ? NST : NST / NW;
     static_assert(rsplit || NST % NW == 0, "super tiles per wave");
+
+    // the first row block's operands, issued ahead of the row loads
+    qi_v2i bA[KS][3], bB[KS][3];
+    int32_t ktA, rsA, ktB, rsB, prA[3], prB[3];
+    const int rlast = RB - 1;
+    const bool single = rb0 + rbs >= RB;
+    load_ops(min(rb0, rlast), bA, ktA, rsA, prA);
 
     // stage the tile as byte planes h' (rows 0..KH-1) and l' (rows KH..):
     // this thread's CPL columns of every RG-th row, all row loads issued back
@@ -1227,7 +1246,7 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
                 // [-1, 65536] either way): no per-element exec masking
 #pragma unroll
                 for (int c = 0; c < 16; c++)
-                    y[c] = fold(fold(mul_i24_s(y[c], rs)));
+                    y[c] = fold(fold(mul_rs(y[c], rs)));
             }
             uint32_t bad = 0;
 #pragma unroll
@@ -1313,17 +1332,20 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     // buffer (or a conditional prefetch) made the compiler drain vmcnt(0) at
     // every row block -- i.e. wait for all the previous block's streaming
     // stores before the next MFMA could issue.
-    qi_v2i bA[KS][3], bB[KS][3];
-    int32_t ktA, rsA, ktB, rsB, prA[3], prB[3];
-    const int rlast = RB - 1;
-    load_ops(min(rb0, rlast), bA, ktA, rsA, prA);
-    for (int rb = rb0; rb < RB; rb += 2 * rbs) {
-        load_ops(min(rb + rbs, rlast), bB, ktB, rsB, prB);
-        rb_body(rb, bA, ktA, rsA, prA);
-        if (rb + rbs >= RB)
-            break;
-        load_ops(min(rb + 2 * rbs, rlast), bA, ktA, rsA, prA);
-        rb_body(rb + rbs, bB, ktB, rsB, prB);
+    if (single) {
+        // one row block for this wave (every decode up to k = 64): its
+        // operands were loaded before the row loads, nothing to prefetch
+        if (rb0 < RB)
+            rb_body(rb0, bA, ktA, rsA, prA);
+    } else {
+        for (int rb = rb0; rb < RB; rb += 2 * rbs) {
+            load_ops(min(rb + rbs, rlast), bB, ktB, rsB, prB);
+            rb_body(rb, bA, ktA, rsA, prA);
+            if (rb + rbs >= RB)
+                break;
+            load_ops(min(rb + 2 * rbs, rlast), bA, ktA, rsA, prA);
+            rb_body(rb + rbs, bB, ktB, rsB, prB);
+        }
     }
     if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
         push_slow_tile(slow, s, col0, NCOL);
@@ -1575,7 +1597,7 @@ matrix_pipe_kernel(MatArgs a, long long n_tiles, int tps)
             if (__builtin_amdgcn_ballot_w64(rs != 1)) {
 #pragma unroll
                 for (int c = 0; c < 16; c++)
-                    y[c] = fold(fold(mul_i24_s(y[c], rs)));
+                    y[c] = fold(fold(mul_rs(y[c], rs)));
             }
             uint32_t bad = 0;
 #pragma unroll

@@ -49,12 +49,25 @@ def test_no_scratch_in_hot_kernels():
     assert not bad, bad
 
 
+def _lds_waves_per_simd(ks, nst, rsplit):
+    """Waves per SIMD the matrix-core kernel's LDS allows (MfmaTile: image
+    2 * 16 KS rows of 64 NST + 16 bytes, mark list, per-wave staging tiles
+    when it has several row blocks; 4 waves per block, 160 KiB per CU)."""
+    img = 2 * 16 * ks * (64 * nst + 16)
+    lds = img + 2 * 4 * 256 + 16 + (4 * 16 * 144 if rsplit or ks > 1 else 0)
+    return min(8, (160 * 1024) // lds)
+
+
 def test_mfma_kernel_occupancy():
-    """The matrix-core kernels for k <= 64 keep >= 4 waves per SIMD (their
-    LDS images allow 4 blocks of 4 waves per CU at k <= 16); the k <= 128
-    kernel (KS = 8, 200 VGPRs) keeps 2."""
+    """The matrix-core kernels keep the occupancy their LDS image allows
+    (registers must not be the tighter limit), and at least 2 waves per
+    SIMD."""
     for k, v in kernels().items():
-        if "matrix_mfma_kernelILi8E" in k or "matrix_mfma_kernelILi16E" in k:
-            assert v.get("Occupancy", 0) >= 2, (k, v)
-        elif "matrix_mfma_kernel" in k:
-            assert v.get("Occupancy", 0) >= 4, (k, v)
+        m = re.search(r"matrix_mfma_kernelILi(\d+)ELi(\d+)ELi4ELb(\d)E", k)
+        if not m:
+            continue
+        ks, nst, rsplit = int(m.group(1)), int(m.group(2)), m.group(3) == "1"
+        want = max(2, min(4, _lds_waves_per_simd(ks, nst, rsplit)))
+        if ks >= 8:
+            want = 2  # 128 < 16 KS rows: 198-248 VGPRs (DESIGN.md 4.2)
+        assert v.get("Occupancy", 0) >= want, (k, v, want)
