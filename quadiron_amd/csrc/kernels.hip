@@ -23,6 +23,32 @@
 #include "matrix_pack.h"
 #include "qi_internal.h"
 
+// timestamp probe of matrix_mfma_kernel (QI_PROBE_TS builds only): per
+// block, s_memrealtime (100 MHz) at entry, after the row loads, after the
+// staging barrier and at exit, plus HW_ID / XCC_ID (tools/mm_ts.py)
+#ifdef QI_PROBE_TS
+__device__ unsigned long long qi_probe_mm[16384][6];
+extern "C" int qi_probe_mm_read(void* host, size_t bytes)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(qi_probe_mm), bytes) == hipSuccess ? 0 : -1;
+}
+#define QI_MM_TS(n)                                                                      \
+    do {                                                                                 \
+        if (threadIdx.x == 0)                                                            \
+            qi_probe_mm[blockIdx.x & 16383][n] = __builtin_amdgcn_s_memrealtime();       \
+    } while (0)
+#define QI_MM_HW()                                                                       \
+    do {                                                                                 \
+        if (threadIdx.x == 0) {                                                          \
+            qi_probe_mm[blockIdx.x & 16383][4] = __builtin_amdgcn_s_getreg(4 | (31 << 11)); \
+            qi_probe_mm[blockIdx.x & 16383][5] = __builtin_amdgcn_s_getreg(20 | (31 << 11)); \
+        }                                                                                \
+    } while (0)
+#else
+#define QI_MM_TS(n) ((void)0)
+#define QI_MM_HW() ((void)0)
+#endif
+
 namespace qi {
 
 constexpr int kBlock = 256;
@@ -630,8 +656,8 @@ __device__ __forceinline__ int scan_tile_marks(const OorScan& sc, long long col0
     return *s_cnt;
 }
 
-template <int KP, int COLS, bool FULL, bool BUF>
-__device__ __forceinline__ void matrix_load(const int (&idv)[2 * KP],
+template <int KP, int COLS, bool FULL, bool BUF, class IdOf>
+__device__ __forceinline__ void matrix_load(const IdOf& id_of,
                                             const RowSrc& src,
                                             const Region<BUF>& g0,
                                             const Region<BUF>& g1, uint32_t voff,
@@ -648,7 +674,7 @@ __device__ __forceinline__ void matrix_load(const int (&idv)[2 * KP],
         uint32_t off[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-            const int id = idv[2 * j + h];
+            const int id = id_of(2 * j + h);
             // branch-free source select (uniform s_cselect): a branch here
             // makes the compiler drain vmcnt after every row load
             const bool lo = id < src.split;
@@ -816,30 +842,54 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(MatArgs a)
         }
     }
 
-    // all ids up front: 2*KP dwords (the context pads past kin), so the
-    // scalar loads batch into a few s_load_dwordxN
-    int idv[2 * KP];
-    if (sid) {
+    // source row of input i: its position (by_pos) or its fragment id; rows
+    // past kin are clamped to a valid row (their coefficients are 0).
+    // KP <= 32: all ids up front in SGPRs (2*KP dwords, the context pads
+    // past kin), so the scalar loads batch into a few s_load_dwordxN.
+    // KP >= 64 (the column tails of k > 64): 128-256 ids do not fit the
+    // SGPRs (they spilled to VGPR lanes and scratch), so lane c of
+    // idl[i / 64] holds id i and the row loads read it with v_readlane.
+    constexpr int NIL = KP >= 64 ? 2 * KP / 64 : 1;
+    constexpr int NIV = KP >= 64 ? 1 : 2 * KP;
+    int idl[NIL];
+    int idv[NIV];
+    if constexpr (KP >= 64) {
+        const int ln = static_cast<int>(threadIdx.x & 63);
 #pragma unroll
-        for (int i = 0; i < 2 * KP; i++)
-            idv[i] = sid[i];
+        for (int c = 0; c < NIL; c++) {
+            const int i = 64 * c + ln;
+            const int ii = i < kin ? i : kin - 1;
+            idl[c] = src.by_pos ? ii : (sid ? sid[i < kin ? i : 0] : (i < kin ? i : 0));
+        }
+        (void)idv;
     } else {
+        (void)idl;
+        if (sid) {
 #pragma unroll
-        for (int i = 0; i < 2 * KP; i++)
-            idv[i] = i;
-    }
+            for (int i = 0; i < 2 * KP; i++)
+                idv[i] = sid[i];
+        } else {
 #pragma unroll
-    for (int i = 0; i < 2 * KP; i++) {
-        // source row of input i: its position (by_pos) or its fragment id;
-        // rows past kin are clamped to a valid row (their coefficients are 0)
-        const int ii = i < kin ? i : kin - 1;
-        idv[i] = src.by_pos ? ii : (i < kin ? idv[i] : idv[0]);
+            for (int i = 0; i < 2 * KP; i++)
+                idv[i] = i;
+        }
+#pragma unroll
+        for (int i = 0; i < 2 * KP; i++) {
+            const int ii = i < kin ? i : kin - 1;
+            idv[i] = src.by_pos ? ii : (i < kin ? idv[i] : idv[0]);
+        }
     }
+    auto id_of = [&](int i) {
+        if constexpr (KP >= 64)
+            return __builtin_amdgcn_readlane(idl[i / 64], i % 64);
+        else
+            return idv[i];
+    };
     int32_t xp[COLS][KP];
     if (full) {
-        matrix_load<KP, COLS, true, BUF>(idv, src, g0, g1, voff, COLS, xp);
+        matrix_load<KP, COLS, true, BUF>(id_of, src, g0, g1, voff, COLS, xp);
     } else if (col < words) {
-        matrix_load<KP, COLS, false, BUF>(idv, src, g0, g1, voff,
+        matrix_load<KP, COLS, false, BUF>(id_of, src, g0, g1, voff,
                                           words - col, xp);
     }
     OorScan sc{in_oor, sid, src.by_pos, slot_base, kin, s, false};
@@ -961,6 +1011,8 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     uint32_t* s_col = reinterpret_cast<uint32_t*>(s_i + kMaxTileOor);
     int* s_cnt = reinterpret_cast<int*>(s_col + kMaxTileOor);
 
+    QI_MM_TS(0);
+    QI_MM_HW();
     int s, tile;
     block_map(blockIdx.x, tiles, s, tile);
     const int kin = L.kin;
@@ -1099,6 +1151,17 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             ld_dw<CPL / 2, true, kAuxLd>(g, off, voff, w[r]);
         }
     }
+#ifdef QI_PROBE_TS
+    {
+        uint32_t dep = 0;
+#pragma unroll
+        for (int r = 0; r < KH / RG; r++)
+            dep |= w[r][0];
+        if (dep == 0x12345678u)
+            qi_probe_mm[0][0] = 0;
+    }
+    QI_MM_TS(1);
+#endif
     const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) +
                           4 * ((cl % 64) / 16) + cl % 4;
 #pragma unroll
@@ -1136,6 +1199,7 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
         __syncthreads();
         n_lm = n_rm;
     }
+    QI_MM_TS(2);
 
     // matrix cores: wave wv covers nst super tiles of 64 columns, for each
     // block of 16 output rows in turn (the next block's operands prefetched)
@@ -1347,6 +1411,10 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             rb_body(rb + rbs, bB, ktB, rsB, prB);
         }
     }
+#ifdef QI_PROBE_TS
+    __syncthreads();
+#endif
+    QI_MM_TS(3);
     if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
         push_slow_tile(slow, s, col0, NCOL);
 }

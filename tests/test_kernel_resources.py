@@ -15,8 +15,9 @@ RES = [os.path.join(ROOT, "build", "obj", f)
 # kernels allowed to use scratch: the adversarial-OOR recompute and the
 # K = 64 encode codelet (256 VGPRs at 2 waves/SIMD, 3-4 spilled registers;
 # 3 waves/SIMD spilled 280 and ran 20 % slower, profiles/r1_ab_k64_encode.txt)
-ALLOWED = ("matrix_redo_kernel", "encode_fnt_kernelILi64E",
-           "matrix_kernelILi64E", "matrix_kernelILi128E")  # dot2 column tails, k > 64
+# (the dot2 column tails of k > 64, matrix_kernel<64|128>, no longer spill:
+# their 128-256 row ids are read from VGPR lanes instead of SGPRs)
+ALLOWED = ("matrix_redo_kernel", "encode_fnt_kernelILi64E")
 
 
 def kernels():
