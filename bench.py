@@ -47,6 +47,7 @@ CONFIGS = {
     "cfg1": (4, 4, 1024, 100),       # the reference's CPU plumbing case
     # larger codes: not BASELINE configs, extra lines.  64 < k <= 256 on
     # the matrix cores, k > 256 on the NTT path
+    "k32": (32, 32, 65536, 1024),    # n = 64: the KS = 2 matrix decode
     "k128": (128, 128, 65536, 128),  # n = 256
     "k200": (200, 56, 65536, 64),    # n = 256
     "k256": (256, 768, 4096, 256),   # n = 1024

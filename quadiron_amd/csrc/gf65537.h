@@ -154,6 +154,36 @@ QI_HD int32_t mul_i24_s(int32_t x, int32_t c)
     return x * sext24(c);
 }
 
+// (w & 0xffff) * c and (w >> 16) * c for a packed pair of u16 columns w and
+// a wave-uniform |c| <= 2^15: one SDWA v_mul_i32_i24 each (the 16-bit
+// half is zero-extended by the operand select, no unpack instruction)
+QI_HD int32_t mul_i24_lo16(uint32_t w, int32_t c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    int32_t r;
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 "
+        "src1_sel:DWORD"
+        : "=v"(r)
+        : "v"(w), "s"(c));
+    return r;
+#else
+    return static_cast<int32_t>(w & 0xffffu) * c;
+#endif
+}
+QI_HD int32_t mul_i24_hi16(uint32_t w, int32_t c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    int32_t r;
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 "
+        "src1_sel:DWORD"
+        : "=v"(r)
+        : "v"(w), "s"(c));
+    return r;
+#else
+    return static_cast<int32_t>(w >> 16) * c;
+#endif
+}
+
 // x * c for a compile-time canonical twiddle c, x in V = [-2, 65537].
 // Result congruent to x*c, range [-32767, 98303] (or T-range pieces for the
 // trivial cases).

@@ -14,9 +14,11 @@
 // BUF=false instantiation (flat global addressing).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "fnt_codelets.h"
 #include "gf65537.h"
@@ -275,6 +277,11 @@ __device__ __forceinline__ void st(const Region<BUF>& g, uint32_t row,
 // one OR-reduction per pass and fixed up off the fast path.
 // KEQ: k == K (no zero-padded inputs to mask).
 // ---------------------------------------------------------------------------
+#ifndef QI_ENC_PAIR
+#define QI_ENC_PAIR 1
+#endif
+static constexpr bool kEncPair = QI_ENC_PAIR != 0;
+
 template <int K, int COLS, bool FULL, bool KEQ, bool BUF>
 __device__ __forceinline__ void encode_body(
     int k, int n, int n_out, const int32_t* __restrict__ twist,
@@ -291,6 +298,7 @@ __device__ __forceinline__ void encode_body(
     constexpr bool RELOAD = K == 32;
     const int passes = n / K;
 
+    constexpr bool PAIR_ = kEncPair && K == 16 && COLS == 2 && FULL;
     int32_t x[COLS][K];
     auto load_x = [&](uint32_t vo) {
 #pragma unroll
@@ -303,7 +311,7 @@ __device__ __forceinline__ void encode_body(
                 x[c][t] = (KEQ || t < k) ? v[c] : 0;
         }
     };
-    if constexpr (!RELOAD)
+    if constexpr (!RELOAD && !PAIR_)
         load_x(voff);
 
     // pass v: y[c][u] = output row passes*u + v of column c, in V = [-2, 65537]
@@ -342,6 +350,12 @@ __device__ __forceinline__ void encode_body(
     // true OOR symbol 65536 or a non-canonical alias) sends the pass through
     // the rare fix-up: canonicalise in place, then record the OOR marks from
     // a bitmask (keeps the atomics out of the unrolled code)
+    // The wave takes the fix-up when any of its lanes has such an output
+    // (about 64 x 2K x 4 / 65537 = 12 % of the passes at K = 16), so the
+    // fix-up is per element and wave-uniform: one compare + ballot per
+    // output, and only the elements some lane has out of range are
+    // canonicalised (the earlier whole-pass canonicalisation with a 64-bit
+    // mark mask cost ~400 instructions per taken pass)
     auto fixup = [&](int v, int32_t (&y)[COLS][K]) {
         uint32_t bad = 0;
 #pragma unroll
@@ -349,25 +363,18 @@ __device__ __forceinline__ void encode_body(
 #pragma unroll
             for (int c = 0; c < COLS; c++)
                 bad |= static_cast<uint32_t>(y[c][u]);
-        if (__builtin_expect((bad >> 16) != 0, 0)) {
-            uint64_t mark = 0;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64((bad >> 16) != 0) != 0, 0)) {
 #pragma unroll
             for (int u = 0; u < K; u++) {
 #pragma unroll
                 for (int c = 0; c < COLS; c++) {
-                    const uint32_t cv = canon_v(y[c][u]);
-                    y[c][u] = static_cast<int32_t>(cv & 0xffffu);
-                    if (cv == 65536u && (FULL || c < avail))
-                        mark |= 1ull << (u * COLS + c);
-                }
-            }
-            if (oor.counts) {
-                while (mark) {
-                    const int bit = __builtin_ctzll(mark);
-                    mark &= mark - 1;
-                    const int row = passes * (bit / COLS) + v;
-                    if (row < n_out)
-                        record_oor(oor, s, row, col + (bit % COLS));
+                    if (__builtin_amdgcn_ballot_w64(static_cast<uint32_t>(y[c][u]) > 65535u)) {
+                        const uint32_t cv = canon_v(y[c][u]);
+                        y[c][u] = static_cast<int32_t>(cv & 0xffffu);
+                        const int row = passes * u + v;
+                        if (cv == 65536u && oor.counts && (FULL || c < avail) && row < n_out)
+                            record_oor(oor, s, row, col + c);
+                    }
                 }
             }
         }
@@ -393,10 +400,92 @@ __device__ __forceinline__ void encode_body(
             }
         }
     };
-    if (n_out >= n)
-        run(std::integral_constant<bool, false>{});
-    else
-        run(std::integral_constant<bool, true>{});
+    // PAIR (K = 16, 2 columns per lane, whole tiles: the cfg2 shape): the
+    // passes run in pairs (v, v + 1) and their stores interleave, rows
+    // 4u + v, 4u + v + 1, ..., so consecutive 256-byte row stores of a wave
+    // alternate the 64 KiB address bit (the pass-order pattern, all 16 rows
+    // of a pass in a row, measured 3.61 ms vs 3.34-3.41 ms for row order /
+    // pass pairs on the bare store pattern, profiles/r1_membw3.txt,
+    // r3_membw4.txt).  The even pass is held packed (16 VGPRs); the inputs
+    // stay packed too (16 VGPRs instead of 32: the twist multiplies read a
+    // column's 16-bit half with SDWA), so the kernel keeps 4 waves per SIMD.
+    auto run_pairs = [&](auto chk) {
+        uint32_t xw[K];
+#pragma unroll
+        for (int t = 0; t < K; t++) {
+            const int row = KEQ ? t : (t < k ? t : k - 1);
+            uint32_t w[1];
+            ld_dw<1, BUF>(gi, static_cast<uint32_t>(row) * irs, voff, w);
+            xw[t] = (KEQ || t < k) ? w[0] : 0u;
+        }
+        auto compute_p = [&](int v, int32_t (&y)[COLS][K]) {
+#pragma unroll
+            for (int t = 0; t < K; t++) {
+                y[0][t] = static_cast<int32_t>(xw[t] & 0xffffu);
+                y[1][t] = static_cast<int32_t>(xw[t] >> 16);
+            }
+            if (v == 0) {
+#pragma unroll
+                for (int c = 0; c < COLS; c++)
+                    dft<K, 0, 65535>(y[c]);
+            } else {
+                const int32_t* tw = twist + v * K;
+#pragma unroll
+                for (int t = 1; t < K; t++) {
+                    const int32_t cb = tw[t];
+                    y[0][t] = fold(mul_i24_lo16(xw[t], cb));
+                    y[1][t] = fold(mul_i24_hi16(xw[t], cb));
+                }
+#pragma unroll
+                for (int c = 0; c < COLS; c++)
+                    dft<K, kTwLo, kTwHi>(y[c]);
+            }
+        };
+        auto packed = [&](int v, uint32_t (&o)[K]) {
+            int32_t y[COLS][K];
+            compute_p(v, y);
+            fixup(v, y);
+#pragma unroll
+            for (int u = 0; u < K; u++)
+                o[u] = pack_lo(static_cast<uint32_t>(y[0][u]), static_cast<uint32_t>(y[1][u]));
+        };
+        auto store = [&](int row, uint32_t o) {
+            if (!decltype(chk)::value || row < n_out) {
+                const uint32_t w[1] = {o};
+                st_dw<1, BUF, kAuxSt>(go, static_cast<uint32_t>(row) * ors, voff, w);
+            }
+        };
+        int v = 0;
+        for (; v + 1 < passes; v += 2) {
+            uint32_t o0[K], o1[K];
+            packed(v, o0);
+            packed(v + 1, o1);
+#pragma unroll
+            for (int u = 0; u < K; u++) {
+                store(passes * u + v, o0[u]);
+                store(passes * u + v + 1, o1[u]);
+            }
+        }
+        if (v < passes) {
+            uint32_t o0[K];
+            packed(v, o0);
+#pragma unroll
+            for (int u = 0; u < K; u++)
+                store(passes * u + v, o0[u]);
+        }
+    };
+    constexpr bool PAIR = kEncPair && K == 16 && COLS == 2 && FULL;
+    if constexpr (PAIR) {
+        if (n_out >= n)
+            run_pairs(std::integral_constant<bool, false>{});
+        else
+            run_pairs(std::integral_constant<bool, true>{});
+    } else {
+        if (n_out >= n)
+            run(std::integral_constant<bool, false>{});
+        else
+            run(std::integral_constant<bool, true>{});
+    }
 }
 
 template <int K, int COLS, bool KEQ, bool BUF>
@@ -949,6 +1038,10 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(MatArgs a)
 // matrix_kernel.
 // ---------------------------------------------------------------------------
 typedef int qi_v4i __attribute__((ext_vector_type(4)));
+#ifndef QI_MM_PIPE
+#define QI_MM_PIPE 1
+#endif
+static constexpr bool kMmPipe = QI_MM_PIPE != 0;
 typedef int qi_v2i __attribute__((ext_vector_type(2)));
 typedef unsigned int qi_v4u __attribute__((ext_vector_type(4)));
 
@@ -1263,12 +1356,11 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
                 }
             }
         };
-        // epilogue + stores of super tile ST from its accumulators
-        auto tile_epi = [&](const int ST, qi_v4i (&acc)[4][3]) {
-            // epilogue: lane (g, t) holds row t, columns cb .. cb + 15;
-            // result j of chunk T is LDS byte 4 g + j = column 16 g + 4 T + j
-            const long long cb = col0 + 64 * ST + 16 * g;
-            int32_t y[16];
+        // epilogue element math of one super tile: lane (g, t) holds row t,
+        // columns 16 g .. 16 g + 15 of the super tile; result j of chunk T is
+        // LDS byte 4 g + j = column 16 g + 4 T + j (straight-line VALU, so
+        // it can share a scheduling region with the next tile's MFMAs)
+        auto tile_y = [&](const qi_v4i (&acc)[4][3], int32_t (&y)[16]) {
 #pragma unroll
             for (int T = 0; T < 4; T++)
 #pragma unroll
@@ -1276,6 +1368,10 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
                     y[4 * T + j] =
                         fold(fold(((KS >= 16 ? fold(acc[T][2][j]) : acc[T][2][j]) << 8) +
                                   acc[T][1][j] - acc[T][0][j]));
+        };
+        // the rest of the epilogue + stores of super tile ST
+        auto tile_fin = [&](const int ST, int32_t (&y)[16]) {
+            const long long cb = col0 + 64 * ST + 16 * g;
             // restored OOR symbols of the received rows: 65536 == -1 where
             // the stored word is 0 (decode_prepare, src/fec_base.h:1361-1404)
             // Branch-free per lane: the marks come from LDS and the
@@ -1380,14 +1476,52 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             __builtin_amdgcn_wave_barrier();
         };
         auto st_of = [&](int st) { return rsplit ? st : wv * nst + st; };
-        // (issuing the next super tile's MFMAs ahead of this epilogue, with
-        // a second accumulator set, measured no gain at KS = 2 or 4:
-        // profiles/r2_ab_pipe.txt)
+        if constexpr (kMmPipe && KS == 4 && nst >= 2 && nst % 2 == 0) {
+            // software pipeline over super-tile pairs: the MFMAs of tile
+            // st + 1 are issued between the element math of tile st (two
+            // accumulator sets), interleaved by sched_group_barrier so the
+            // matrix pipe runs under the epilogue's VALU instead of after it
+            constexpr int NMF = 4 * (KS == 2 ? 3 : 3 * KS / 2 - KS / 2);  // MFMAs per tile
+            constexpr int NDS = 4 * KS;                                   // A reads per tile
+            constexpr int VPM = (KS >= 16 ? 80 : 64) / NMF;               // VALU per MFMA
+            qi_v4i a0[4][3], a1[4][3];
+            auto interleave = [&]() {
+                __builtin_amdgcn_sched_group_barrier(0x100, NDS, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+#pragma unroll
+                for (int i = 0; i < NMF; i++) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
+                }
+            };
+            auto pair = [&](int st, auto last_c) {
+                constexpr bool last = decltype(last_c)::value;
+                int32_t y[16];
+                tile_mfma(st_of(st + 1), a1);
+                tile_y(a0, y);
+                interleave();
+                tile_fin(st_of(st), y);
+                if constexpr (!last)
+                    tile_mfma(st_of(st + 2), a0);
+                tile_y(a1, y);
+                if constexpr (!last)
+                    interleave();
+                tile_fin(st_of(st + 1), y);
+            };
+            tile_mfma(st_of(0), a0);
 #pragma unroll 1
-        for (int st = 0; st < nst; st++) {
-            qi_v4i acc[4][3];
-            tile_mfma(st_of(st), acc);
-            tile_epi(st_of(st), acc);
+            for (int st = 0; st < nst - 2; st += 2)
+                pair(st, std::false_type{});
+            pair(nst - 2, std::true_type{});
+        } else {
+#pragma unroll 1
+            for (int st = 0; st < nst; st++) {
+                qi_v4i acc[4][3];
+                int32_t y[16];
+                tile_mfma(st_of(st), acc);
+                tile_y(acc, y);
+                tile_fin(st_of(st), y);
+            }
         }
     };
     // Row blocks in ping-pong over two operand buffers, each prefetch one row
@@ -1417,6 +1551,341 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     QI_MM_TS(3);
     if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
         push_slow_tile(slow, s, col0, NCOL);
+}
+
+// ---------------------------------------------------------------------------
+// Operand-stationary matrix-core kernel for long matrices (KS = 8, 16:
+// 64 < kin <= 256; the decodes and generators of k = 65 .. 256).
+//
+// matrix_mfma_kernel re-fetches every row block's operand tiles (16 KB of
+// non-zero i8 tiles per 16 output rows at KS = 16) for every 64-column block,
+// so its operand stream from L2 was ~8x the HBM data stream and the kernel
+// ran at 0.8-1 TB/s (k = 200, 256).  Here every wave owns ONE row block for
+// the block's whole life: its operand tiles stay in registers (KS / 2 + KS / 4
+// + KS / 4 v4i, 64 VGPRs at KS = 16), and the block streams a range of
+// 64-column tiles of one stripe through a double-buffered byte-plane image
+// (the next tile's rows are loaded into registers while this one is on the
+// matrix cores).  8 waves per block cover 8 row blocks (interleaved: group
+// gq of G takes rb = gq, gq + G, ...); a matrix with more row blocks runs G
+// blocks per column range, which read the same input tiles (L2 hits: the
+// XCD-aware map puts them on one XCD).
+// The arithmetic, operand tiles, epilogue and OOR handling are
+// matrix_mfma_kernel's (byte split, 2^16 = -1, D2 folded first at KS = 16).
+// ---------------------------------------------------------------------------
+template <int KS>
+struct OsTile {
+    static constexpr int kWaves = 8;
+    static constexpr int kThreads = 64 * kWaves;
+    static constexpr int kRows = 16 * KS;      // rows per byte plane (KH)
+    static constexpr int kPitch = 64 + 16;     // LDS row pitch: +4 banks/row
+    static constexpr size_t kImg = static_cast<size_t>(2 * kRows) * kPitch;
+    static constexpr int kStagePitch = 144;
+    static constexpr size_t kStage = 16 * kStagePitch;
+    static constexpr size_t kStageOff = 2 * kImg;
+    static constexpr size_t kMarkOff = kStageOff + kWaves * kStage;
+    // two mark lists (s_i, s_col) + two counts
+    static constexpr size_t kLds = kMarkOff + 2 * 2 * 4 * kMaxTileOor + 16;
+    // staging: 16 lanes x 4 columns per image row, 32 rows per pass
+    static constexpr int kRpt = kRows / 32;  // rows per thread
+};
+
+template <int KS, bool TWO>
+__global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C, int TS)
+{
+    using O = OsTile<KS>;
+    constexpr int KH = O::kRows, RSB = O::kPitch, RPT = O::kRpt;
+    extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
+    const MatLayout L = a.L;
+    const RowSrc src = a.src;
+    const RowDst dst = a.dst;
+    const MatExt ext = a.ext;
+    const Oor in_oor = a.in_oor;
+    const Oor out_oor = a.out_oor;
+    const int kin = L.kin;
+    const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+    const int g = l >> 4, q = (l & 15) >> 1, p = l & 1, tl = l & 15;
+
+    // block -> (stripe, row-block group, column range); the G groups of one
+    // (stripe, range) on the same XCD when the units tile the 8 XCDs
+    int s, gq, cr;
+    {
+        const int L0 = blockIdx.x;
+        int unit;
+        const int S = static_cast<int>(gridDim.x) / (G * C);
+        if (((S * C) & 7) == 0) {
+            const int x = L0 & 7, j = L0 >> 3;
+            gq = j % G;
+            unit = (j / G) * 8 + x;
+        } else {
+            gq = L0 % G;
+            unit = L0 / G;
+        }
+        s = unit / C;
+        cr = unit - s * C;
+    }
+    const int t0 = static_cast<int>(static_cast<long long>(cr) * TS / C);
+    const int t1 = static_cast<int>(static_cast<long long>(cr + 1) * TS / C);
+
+    const int RB = L.RB();
+    const int rb = gq + G * wv;
+    const bool act = rb < RB;  // wave-uniform
+    const int rbc = act ? rb : RB - 1;
+    const int32_t* M = a.mat + s * a.ms;
+    const int32_t* mf = M + L.mf();
+    const int32_t* kmf = M + L.kmf();
+    const int32_t* rscale = M + L.rscale_mf();
+    const int32_t* plain = M + L.plain();
+    const int32_t* __restrict__ rowmap = a.rowmap;
+    const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
+
+    // this wave's operand tiles, for the block's whole life: [a|0] over the
+    // h' K-steps, [0|b] over the l' K-steps, [b|a] over all (x64 pairs)
+    qi_v4i b0[KS / 4], b1[KS / 4], b2[KS / 2];
+    {
+        auto ld2 = [&](int ks, int ty) {
+            return *reinterpret_cast<const qi_v2i*>(mf + ((rbc * KS + ks) * 3 + ty) * 128 + l * 2);
+        };
+#pragma unroll
+        for (int i = 0; i < KS / 4; i++) {
+            const qi_v2i x0 = ld2(2 * i, 0), x1 = ld2(2 * i + 1, 0);
+            b0[i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
+            const qi_v2i y0 = ld2(KS / 2 + 2 * i, 1), y1 = ld2(KS / 2 + 2 * i + 1, 1);
+            b1[i] = qi_v4i{y0.x, y0.y, y1.x, y1.y};
+        }
+#pragma unroll
+        for (int i = 0; i < KS / 2; i++) {
+            const qi_v2i x0 = ld2(2 * i, 2), x1 = ld2(2 * i + 1, 2);
+            b2[i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
+        }
+    }
+    const int t = 16 * rbc + tl;
+    const bool trow = act && t < L.R;
+    const int tcl = t < L.R ? t : L.R - 1;
+    const int32_t kt = t < L.R ? kmf[tcl] : 0;
+    const int32_t rs = t < L.R ? rscale[tcl] : 1;
+    int32_t pr[3];
+    pr[0] = rowmap[tcl];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int ot = 16 * rbc + 8 * h + (l >> 3);
+        pr[1 + h] = rowmap[ot < L.R ? ot : L.R - 1];
+    }
+
+    // staging: lane (rowgrp, cl) loads 4 columns (b64) of rows 32 r + rowgrp;
+    // per-lane row offsets fixed for the block (rows past kin clamped: their
+    // operand bytes are 0).  TWO (two source regions, systematic decodes):
+    // both regions are loaded with an out-of-range offset for the region
+    // the row is not in (the hardware returns 0) and OR-ed.
+    const Region<true> g0(src.base0 + s * src.ss0, ext.e0);
+    const Region<true> g1(src.base1 ? src.base1 + s * src.ss1 : src.base0, ext.e1);
+    const Region<true> go(dst.base + s * dst.ss, ext.eo);
+    const int rowgrp = tid >> 4, cl = (tid & 15) * 4;
+    constexpr uint32_t kOob = 0x80000000u;  // past any extent (< 2^31)
+    uint32_t off0[RPT], off1[TWO ? RPT : 1];
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+        const int i = 32 * r + rowgrp;
+        const int ii = i < kin ? i : kin - 1;
+        const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
+        const uint32_t lane = static_cast<uint32_t>(cl * 2);
+        if constexpr (TWO) {
+            const bool lo = id < src.split;
+            off0[r] = lo ? static_cast<uint32_t>(id * src.rs0 * 2) + lane : kOob;
+            off1[r] = lo ? kOob : static_cast<uint32_t>((id - src.split) * src.rs1 * 2) + lane;
+        } else {
+            off0[r] = static_cast<uint32_t>(id * src.rs0 * 2) + lane;
+        }
+    }
+    uint32_t w[RPT][2];
+    auto issue_rows = [&](int tile) {
+        const int so = tile * 128;  // byte offset of the tile's first column
+#pragma unroll
+        for (int r = 0; r < RPT; r++) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(g0.r, static_cast<int>(off0[r]),
+                                                                so, kAuxLd);
+            w[r][0] = v[0];
+            w[r][1] = v[1];
+            if constexpr (TWO) {
+                const auto u = __builtin_amdgcn_raw_buffer_load_b64(
+                    g1.r, static_cast<int>(off1[r]), so, kAuxLd);
+                w[r][0] |= u[0];
+                w[r][1] |= u[1];
+            }
+        }
+    };
+    const uint32_t lpos = 16 * ((cl % 16) / 4) + 4 * (cl / 16);
+    auto write_rows = [&](uint8_t* img) {
+#pragma unroll
+        for (int r = 0; r < RPT; r++) {
+            const int i = 32 * r + rowgrp;
+            const uint32_t hi = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x07050301u) ^ 0x80808080u;
+            const uint32_t lo = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x06040200u) ^ 0x80808080u;
+            *reinterpret_cast<uint32_t*>(img + i * RSB + lpos) = hi;
+            *reinterpret_cast<uint32_t*>(img + (KH + i) * RSB + lpos) = lo;
+        }
+    };
+
+    // OOR marks of the received rows in a tile (route table or bucket
+    // scan) into mark list mb; returns the count (all threads)
+    auto s_i = [&](int mb) {
+        return reinterpret_cast<int*>(qi_lds + O::kMarkOff) + mb * 2 * kMaxTileOor;
+    };
+    auto s_col = [&](int mb) { return reinterpret_cast<uint32_t*>(s_i(mb) + kMaxTileOor); };
+    auto s_cnt = [&](int mb) {
+        return reinterpret_cast<int*>(qi_lds + O::kMarkOff + 2 * 2 * 4 * kMaxTileOor) + mb;
+    };
+    const bool marks_in = in_oor.counts != nullptr;
+    auto stage_marks = [&](int tile, int mb) -> int {
+        if (!marks_in)
+            return 0;
+        const long long col0 = static_cast<long long>(tile) * 64;
+        if (a.route) {
+            const uint32_t* rt = a.route + s * a.rstride + (col0 / kRouteTile) * kRouteStride;
+            const uint32_t rc = rt[0];
+            if (rc <= static_cast<uint32_t>(kRouteCap)) {
+                stage_route_marks(rt + 1, static_cast<int>(rc), col0, s_i(mb), s_col(mb));
+                return static_cast<int>(rc);
+            }
+        }
+        OorScan sc{in_oor, sid, src.by_pos, a.slot_base, kin, s, false};
+        const int cnt = scan_tile_marks(sc, col0, col0 + 64, a.words, s_cnt(mb), s_i(mb),
+                                        s_col(mb), a.err);
+        if (cnt > kMaxTileOor && tid == 0)  // rare: see matrix_redo_kernel
+            push_slow_tile(a.slow, s, col0, 64);
+        return min(cnt, kMaxTileOor);
+    };
+
+    const bool rec = out_oor.counts != nullptr;
+    const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
+    const uint32_t abase = static_cast<uint32_t>((8 * g + q) * RSB + 8 * p);
+    uint8_t* stg = qi_lds + O::kStageOff + wv * O::kStage;
+
+    // one tile: the wave's 16 x 64 output block from image img
+    auto compute = [&](const uint8_t* img, long long col0, int n_lm, const int* mi,
+                       const uint32_t* mc) {
+        auto* lds = (__attribute__((address_space(3))) const uint8_t*)img;
+        qi_v4i acc[4][3];
+#pragma unroll
+        for (int T = 0; T < 4; T++) {
+            qi_v4i av[KS / 2];
+#pragma unroll
+            for (int i = 0; i < KS / 2; i++) {
+                auto rd = [&](int ks) {
+                    auto* pa = (__attribute__((address_space(3))) qi_v2i*)(
+                        lds + abase + 32 * ks * RSB + T * 16);
+                    return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
+                };
+                const qi_v2i x0 = rd(2 * i), x1 = rd(2 * i + 1);
+                av[i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
+            }
+            acc[T][0] = qi_v4i{0, 0, 0, 0};
+            acc[T][1] = qi_v4i{kt, kt, kt, kt};
+            acc[T][2] = qi_v4i{0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < KS / 4; i++) {
+                acc[T][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b0[i], acc[T][0], 0, 0, 0);
+                acc[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[KS / 4 + i], b1[i], acc[T][1],
+                                                                  0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < KS / 2; i++)
+                acc[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b2[i], acc[T][2], 0, 0, 0);
+        }
+        // epilogue: lane (g, t) holds row t, columns cb .. cb + 15
+        const long long cb = col0 + 16 * g;
+        int32_t y[16];
+#pragma unroll
+        for (int T = 0; T < 4; T++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                y[4 * T + j] = fold(fold(((KS >= 16 ? fold(acc[T][2][j]) : acc[T][2][j]) << 8) +
+                                         acc[T][1][j] - acc[T][0][j]));
+        // restored OOR symbols of the received rows (decode_prepare,
+        // src/fec_base.h:1361-1404): 65536 == -1 where the stored word is 0
+        const uint32_t st0 = static_cast<uint32_t>(col0);
+        for (int e = 0; e < n_lm; e++) {
+            const uint32_t wcu = __builtin_amdgcn_readfirstlane(mc[e]);
+            if (wcu - st0 >= 64u)
+                continue;
+            const int pos = __builtin_amdgcn_readfirstlane(mi[e]);
+            const long long d = static_cast<long long>(wcu) - cb;
+            const int32_t corr = plain[tcl * kin + pos];
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                const int32_t yc = fold(fold(y[c] - corr));
+                y[c] = (trow && d == c) ? yc : y[c];
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(rs != 1)) {
+#pragma unroll
+            for (int c = 0; c < 16; c++)
+                y[c] = fold(fold(mul_rs(y[c], rs)));
+        }
+        uint32_t bad = 0;
+#pragma unroll
+        for (int c = 0; c < 16; c++)
+            bad |= static_cast<uint32_t>(y[c]);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64((bad >> 16) != 0) != 0, 0)) {
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                if (static_cast<uint32_t>(y[c]) > 65535u) {
+                    if (rec && trow)
+                        record_oor(out_oor, s, pr[0], cb + c);
+                    y[c] = 0;  // 65536 (or its alias -1) is stored as 0
+                }
+            }
+        }
+        qi_v4u o0, o1;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            o0[c] = pack_lo(static_cast<uint32_t>(y[2 * c]), static_cast<uint32_t>(y[2 * c + 1]));
+            o1[c] = pack_lo(static_cast<uint32_t>(y[8 + 2 * c]),
+                            static_cast<uint32_t>(y[8 + 2 * c + 1]));
+        }
+        // transposed through the wave's staging tile into whole-line stores
+        *reinterpret_cast<qi_v4u*>(stg + tl * O::kStagePitch + 32 * g) = o0;
+        *reinterpret_cast<qi_v4u*>(stg + tl * O::kStagePitch + 32 * g + 16) = o1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int orow = 8 * h + (l >> 3), c = l & 7;
+            const qi_v4u v =
+                *reinterpret_cast<const qi_v4u*>(stg + orow * O::kStagePitch + 16 * c);
+            const int ot = 16 * rbc + orow;
+            const uint32_t vo = ot < L.R ? static_cast<uint32_t>(pr[1 + h]) * ors +
+                                               static_cast<uint32_t>((col0 + 8 * c) * 2)
+                                         : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo), 0, kAuxStMf);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    };
+
+    if (t0 >= t1)
+        return;
+    auto img = [&](int b) { return qi_lds + b * O::kImg; };
+    issue_rows(t0);
+    write_rows(img(0));
+    int nl[2];
+    nl[0] = stage_marks(t0, 0);
+    nl[1] = 0;
+    __syncthreads();
+#pragma unroll 1
+    for (int tile = t0; tile < t1; tile++) {
+        const int b = (tile - t0) & 1;
+        const bool more = tile + 1 < t1;  // block-uniform
+        if (more)
+            issue_rows(tile + 1);
+        if (act)
+            compute(img(b), static_cast<long long>(tile) * 64, nl[b], s_i(b), s_col(b));
+        if (more) {
+            write_rows(img(b ^ 1));
+            nl[b ^ 1] = stage_marks(tile + 1, b ^ 1);
+        }
+        __syncthreads();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1921,9 +2390,66 @@ static bool pipe_enabled()
     return matk_mode() == 1;
 }
 
+// operand-stationary kernel (KS = 8, 16): G row-block groups of 8 waves, C
+// column ranges per stripe; about two blocks per CU over the launch
+#ifndef QI_MM_OS
+#define QI_MM_OS 1
+#endif
+static constexpr bool kMmOs = QI_MM_OS != 0;
+
+template <int KS>
+static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
+{
+    using O = OsTile<KS>;
+    const long long TS = wfull / 64;
+    if (TS <= 0 || TS > 0x7fffffffLL)
+        return -1;
+    const int RB = a.L.RB();
+    const int G = (RB + O::kWaves - 1) / O::kWaves;
+    long long C = (512 + static_cast<long long>(S) * G - 1) / (static_cast<long long>(S) * G);
+    C = std::max(1LL, std::min(C, std::max(1LL, TS / 4)));
+    // the XCD map wants S * C a multiple of 8
+    while ((S * C) % 8 != 0 && C < TS / 2)
+        C++;
+    const long long blocks = static_cast<long long>(S) * G * C;
+    if (blocks > 0x7fffffffLL)
+        return -1;
+    static std::atomic<uint64_t> attr_done{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return -2;
+    const uint64_t bit = dev < 64 ? 1ull << dev : 0;
+    const bool two = a.src.base1 != nullptr;
+    const void* fn = two ? reinterpret_cast<const void*>(&matrix_os_kernel<KS, true>)
+                         : reinterpret_cast<const void*>(&matrix_os_kernel<KS, false>);
+    if (O::kLds > 65536 && (!bit || !(attr_done.load(std::memory_order_acquire) & bit))) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&matrix_os_kernel<KS, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(O::kLds)) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&matrix_os_kernel<KS, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(O::kLds)) != hipSuccess)
+            return -2;
+        attr_done.fetch_or(bit, std::memory_order_release);
+    }
+    (void)fn;
+    a.tiles = static_cast<int>(TS);
+    if (two)
+        hipLaunchKernelGGL((matrix_os_kernel<KS, true>), dim3(static_cast<unsigned>(blocks)),
+                           dim3(O::kThreads), O::kLds, st, a, G, static_cast<int>(C),
+                           static_cast<int>(TS));
+    else
+        hipLaunchKernelGGL((matrix_os_kernel<KS, false>), dim3(static_cast<unsigned>(blocks)),
+                           dim3(O::kThreads), O::kLds, st, a, G, static_cast<int>(C),
+                           static_cast<int>(TS));
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 template <int KS>
 static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t st)
 {
+    if constexpr (kMmOs && (KS == 8 || KS == 16))
+        return os_launch<KS>(a, wfull, S, st);
     constexpr int NSTS = KS == 1 ? 16 : 8;
     const int RB = a.L.RB();
     if constexpr (KS == 16) {
@@ -2056,8 +2582,11 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
             nst = 4;
             rsplit = true;
         }
-        r = "matrix_mfma_kernel<" + std::to_string(KS) + "," + std::to_string(nst) + "," +
-            std::to_string(nw) + "," + (rsplit ? "true" : "false") + ">";
+        if (kMmOs && (KS == 8 || KS == 16))
+            r = "matrix_os_kernel<" + std::to_string(KS) + ">";
+        else
+            r = "matrix_mfma_kernel<" + std::to_string(KS) + "," + std::to_string(nst) + "," +
+                std::to_string(nw) + "," + (rsplit ? "true" : "false") + ">";
     }
     if (wfull < words) {
         const int cols = L.KP <= 8 ? 4 : L.KP <= 16 ? 2 : 1;
