@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <string>
 #include <type_traits>
+#include <utility>
 
 #include "fnt_codelets.h"
 #include "gf65537.h"
@@ -1554,30 +1555,36 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// Operand-stationary matrix-core kernel for long matrices (KS = 8, 16:
-// 64 < kin <= 256; the decodes and generators of k = 65 .. 256).
+// Operand-stationary matrix-core kernel (KS = 4, 8, 16: 32 < kin <= 256; the
+// decodes of k = 33 .. 256 and the generators of those codes).
 //
-// matrix_mfma_kernel re-fetches every row block's operand tiles (16 KB of
-// non-zero i8 tiles per 16 output rows at KS = 16) for every 64-column block,
-// so its operand stream from L2 was ~8x the HBM data stream and the kernel
-// ran at 0.8-1 TB/s (k = 200, 256).  Here every wave owns ONE row block for
-// the block's whole life: its operand tiles stay in registers (KS / 2 + KS / 4
-// + KS / 4 v4i, 64 VGPRs at KS = 16), and the block streams a range of
-// 64-column tiles of one stripe through a double-buffered byte-plane image
-// (the next tile's rows are loaded into registers while this one is on the
-// matrix cores).  8 waves per block cover 8 row blocks (interleaved: group
-// gq of G takes rb = gq, gq + G, ...); a matrix with more row blocks runs G
-// blocks per column range, which read the same input tiles (L2 hits: the
-// XCD-aware map puts them on one XCD).
+// matrix_mfma_kernel stages one column block, computes it and exits: every
+// block re-fetches the operand tiles of every row block it covers from L2
+// (16 KB of non-zero i8 tiles per 16 output rows at KS = 16, ~8x the HBM
+// data stream at k = 200), and its load and compute phases run one after
+// the other (two blocks per CU in lock step).  Here a block of 8 waves
+// stays on one stripe for a range of column tiles:
+//   - wave w owns RPW row blocks (slot w % WR) for the block's whole life:
+//     their operand tiles stay in registers (KS / 2 + KS / 2 v4i each: 64
+//     VGPRs at KS = 16), with kmf / rscale / rowmap;
+//   - a tile is 64 NSTT columns, NSTT = 8 / WR super tiles of 64 columns
+//     (wave w takes super tile w / WR), staged as the byte-plane image of
+//     matrix_mfma_kernel in one of two LDS buffers: the next tile's rows are
+//     loaded into registers while this one is on the matrix cores;
+//   - a matrix with more than WR RPW row blocks runs G blocks per column
+//     range (group gq takes rb = gq WR RPW + slot + WR j); they read the same
+//     input tiles, and the XCD-aware map puts them on one XCD (shared L2).
 // The arithmetic, operand tiles, epilogue and OOR handling are
 // matrix_mfma_kernel's (byte split, 2^16 = -1, D2 folded first at KS = 16).
 // ---------------------------------------------------------------------------
-template <int KS>
+template <int KS, int WR>
 struct OsTile {
     static constexpr int kWaves = 8;
     static constexpr int kThreads = 64 * kWaves;
+    static constexpr int kNst = kWaves / WR;   // super tiles per tile
+    static constexpr int kCols = 64 * kNst;    // columns per tile
     static constexpr int kRows = 16 * KS;      // rows per byte plane (KH)
-    static constexpr int kPitch = 64 + 16;     // LDS row pitch: +4 banks/row
+    static constexpr int kPitch = kCols + 16;  // LDS row pitch: +4 banks/row
     static constexpr size_t kImg = static_cast<size_t>(2 * kRows) * kPitch;
     static constexpr int kStagePitch = 144;
     static constexpr size_t kStage = 16 * kStagePitch;
@@ -1585,15 +1592,19 @@ struct OsTile {
     static constexpr size_t kMarkOff = kStageOff + kWaves * kStage;
     // two mark lists (s_i, s_col) + two counts
     static constexpr size_t kLds = kMarkOff + 2 * 2 * 4 * kMaxTileOor + 16;
-    // staging: 16 lanes x 4 columns per image row, 32 rows per pass
-    static constexpr int kRpt = kRows / 32;  // rows per thread
+    // staging: 4 columns (b64) per lane, kTpr lanes per image row
+    static constexpr int kTpr = kCols / 4;
+    static constexpr int kRpp = kThreads / kTpr;  // rows per pass
+    static constexpr int kRpt = kRows / kRpp;     // rows per thread
+    static_assert(kRpt >= 1 && kRows % kRpp == 0, "staging");
 };
 
-template <int KS, bool TWO>
+template <int KS, int WR, int RPW, bool TWO>
 __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C, int TS)
 {
-    using O = OsTile<KS>;
-    constexpr int KH = O::kRows, RSB = O::kPitch, RPT = O::kRpt;
+    using O = OsTile<KS, WR>;
+    constexpr int KH = O::kRows, RSB = O::kPitch, RPT = O::kRpt, NCOL = O::kCols;
+    static_assert(KS == 4 || KS == 8 || KS == 16, "x64 pairs with zero halves");
     extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
     const MatLayout L = a.L;
     const RowSrc src = a.src;
@@ -1627,9 +1638,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     const int t1 = static_cast<int>(static_cast<long long>(cr + 1) * TS / C);
 
     const int RB = L.RB();
-    const int rb = gq + G * wv;
-    const bool act = rb < RB;  // wave-uniform
-    const int rbc = act ? rb : RB - 1;
+    const int slot = wv % WR, st = wv / WR;  // row-block slot, super tile
     const int32_t* M = a.mat + s * a.ms;
     const int32_t* mf = M + L.mf();
     const int32_t* kmf = M + L.kmf();
@@ -1638,53 +1647,61 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     const int32_t* __restrict__ rowmap = a.rowmap;
     const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
 
-    // this wave's operand tiles, for the block's whole life: [a|0] over the
-    // h' K-steps, [0|b] over the l' K-steps, [b|a] over all (x64 pairs)
-    qi_v4i b0[KS / 4], b1[KS / 4], b2[KS / 2];
-    {
+    // this wave's row blocks and their operand tiles, for the block's whole
+    // life: [a|0] over the h' K-steps, [0|b] over the l' K-steps, [b|a] over
+    // all (x64 pairs)
+    int rbj[RPW];
+    bool act[RPW];
+    qi_v4i b0[RPW][KS / 4], b1[RPW][KS / 4], b2[RPW][KS / 2];
+    int32_t kt[RPW], rs[RPW], pr[RPW][3];
+#pragma unroll
+    for (int j = 0; j < RPW; j++) {
+        const int rb = gq * WR * RPW + slot + WR * j;
+        act[j] = rb < RB;  // wave-uniform
+        const int rbc = act[j] ? rb : RB - 1;
+        rbj[j] = rbc;
         auto ld2 = [&](int ks, int ty) {
             return *reinterpret_cast<const qi_v2i*>(mf + ((rbc * KS + ks) * 3 + ty) * 128 + l * 2);
         };
 #pragma unroll
         for (int i = 0; i < KS / 4; i++) {
             const qi_v2i x0 = ld2(2 * i, 0), x1 = ld2(2 * i + 1, 0);
-            b0[i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
+            b0[j][i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
             const qi_v2i y0 = ld2(KS / 2 + 2 * i, 1), y1 = ld2(KS / 2 + 2 * i + 1, 1);
-            b1[i] = qi_v4i{y0.x, y0.y, y1.x, y1.y};
+            b1[j][i] = qi_v4i{y0.x, y0.y, y1.x, y1.y};
         }
 #pragma unroll
         for (int i = 0; i < KS / 2; i++) {
             const qi_v2i x0 = ld2(2 * i, 2), x1 = ld2(2 * i + 1, 2);
-            b2[i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
+            b2[j][i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
+        }
+        const int t = 16 * rbc + tl;
+        const int tcl = t < L.R ? t : L.R - 1;
+        const int32_t k0 = kmf[tcl], r0 = rscale[tcl];
+        kt[j] = t < L.R ? k0 : 0;
+        rs[j] = t < L.R ? r0 : 1;
+        pr[j][0] = rowmap[tcl];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int ot = 16 * rbc + 8 * h + (l >> 3);
+            pr[j][1 + h] = rowmap[ot < L.R ? ot : L.R - 1];
         }
     }
-    const int t = 16 * rbc + tl;
-    const bool trow = act && t < L.R;
-    const int tcl = t < L.R ? t : L.R - 1;
-    const int32_t kt = t < L.R ? kmf[tcl] : 0;
-    const int32_t rs = t < L.R ? rscale[tcl] : 1;
-    int32_t pr[3];
-    pr[0] = rowmap[tcl];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int ot = 16 * rbc + 8 * h + (l >> 3);
-        pr[1 + h] = rowmap[ot < L.R ? ot : L.R - 1];
-    }
 
-    // staging: lane (rowgrp, cl) loads 4 columns (b64) of rows 32 r + rowgrp;
-    // per-lane row offsets fixed for the block (rows past kin clamped: their
-    // operand bytes are 0).  TWO (two source regions, systematic decodes):
-    // both regions are loaded with an out-of-range offset for the region
-    // the row is not in (the hardware returns 0) and OR-ed.
+    // staging: lane (rowgrp, cl) loads 4 columns (b64) of rows kRpp r +
+    // rowgrp; per-lane row offsets fixed for the block (rows past kin
+    // clamped: their operand bytes are 0).  TWO (two source regions,
+    // systematic decodes): both regions are loaded, with an out-of-range
+    // offset in the region the row is not in (the hardware returns 0).
     const Region<true> g0(src.base0 + s * src.ss0, ext.e0);
     const Region<true> g1(src.base1 ? src.base1 + s * src.ss1 : src.base0, ext.e1);
     const Region<true> go(dst.base + s * dst.ss, ext.eo);
-    const int rowgrp = tid >> 4, cl = (tid & 15) * 4;
+    const int rowgrp = tid / O::kTpr, cl = (tid % O::kTpr) * 4;
     constexpr uint32_t kOob = 0x80000000u;  // past any extent (< 2^31)
     uint32_t off0[RPT], off1[TWO ? RPT : 1];
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
-        const int i = 32 * r + rowgrp;
+        const int i = O::kRpp * r + rowgrp;
         const int ii = i < kin ? i : kin - 1;
         const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
         const uint32_t lane = static_cast<uint32_t>(cl * 2);
@@ -1698,7 +1715,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     }
     uint32_t w[RPT][2];
     auto issue_rows = [&](int tile) {
-        const int so = tile * 128;  // byte offset of the tile's first column
+        const int so = tile * NCOL * 2;  // byte offset of the tile's first column
 #pragma unroll
         for (int r = 0; r < RPT; r++) {
             const auto v = __builtin_amdgcn_raw_buffer_load_b64(g0.r, static_cast<int>(off0[r]),
@@ -1713,11 +1730,11 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             }
         }
     };
-    const uint32_t lpos = 16 * ((cl % 16) / 4) + 4 * (cl / 16);
+    const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) + 4 * ((cl % 64) / 16);
     auto write_rows = [&](uint8_t* img) {
 #pragma unroll
         for (int r = 0; r < RPT; r++) {
-            const int i = 32 * r + rowgrp;
+            const int i = O::kRpp * r + rowgrp;
             const uint32_t hi = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x07050301u) ^ 0x80808080u;
             const uint32_t lo = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x06040200u) ^ 0x80808080u;
             *reinterpret_cast<uint32_t*>(img + i * RSB + lpos) = hi;
@@ -1738,7 +1755,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     auto stage_marks = [&](int tile, int mb) -> int {
         if (!marks_in)
             return 0;
-        const long long col0 = static_cast<long long>(tile) * 64;
+        const long long col0 = static_cast<long long>(tile) * NCOL;
         if (a.route) {
             const uint32_t* rt = a.route + s * a.rstride + (col0 / kRouteTile) * kRouteStride;
             const uint32_t rc = rt[0];
@@ -1748,22 +1765,27 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             }
         }
         OorScan sc{in_oor, sid, src.by_pos, a.slot_base, kin, s, false};
-        const int cnt = scan_tile_marks(sc, col0, col0 + 64, a.words, s_cnt(mb), s_i(mb),
+        const int cnt = scan_tile_marks(sc, col0, col0 + NCOL, a.words, s_cnt(mb), s_i(mb),
                                         s_col(mb), a.err);
         if (cnt > kMaxTileOor && tid == 0)  // rare: see matrix_redo_kernel
-            push_slow_tile(a.slow, s, col0, 64);
+            push_slow_tile(a.slow, s, col0, NCOL);
         return min(cnt, kMaxTileOor);
     };
 
     const bool rec = out_oor.counts != nullptr;
     const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
-    const uint32_t abase = static_cast<uint32_t>((8 * g + q) * RSB + 8 * p);
+    const uint32_t abase = static_cast<uint32_t>((8 * g + q) * RSB + 8 * p + 64 * st);
     uint8_t* stg = qi_lds + O::kStageOff + wv * O::kStage;
 
-    // one tile: the wave's 16 x 64 output block from image img
+    // row block j of this wave over its super tile (columns col0 ..
+    // col0 + 63) from image img
     auto compute = [&](const uint8_t* img, long long col0, int n_lm, const int* mi,
-                       const uint32_t* mc) {
+                       const uint32_t* mc, auto jc) {
+        constexpr int j = decltype(jc)::value;
         auto* lds = (__attribute__((address_space(3))) const uint8_t*)img;
+        const int t = 16 * rbj[j] + tl;
+        const bool trow = act[j] && t < L.R;
+        const int tcl = t < L.R ? t : L.R - 1;
         qi_v4i acc[4][3];
 #pragma unroll
         for (int T = 0; T < 4; T++) {
@@ -1779,17 +1801,19 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
                 av[i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
             }
             acc[T][0] = qi_v4i{0, 0, 0, 0};
-            acc[T][1] = qi_v4i{kt, kt, kt, kt};
+            acc[T][1] = qi_v4i{kt[j], kt[j], kt[j], kt[j]};
             acc[T][2] = qi_v4i{0, 0, 0, 0};
 #pragma unroll
             for (int i = 0; i < KS / 4; i++) {
-                acc[T][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b0[i], acc[T][0], 0, 0, 0);
-                acc[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[KS / 4 + i], b1[i], acc[T][1],
-                                                                  0, 0, 0);
+                acc[T][0] =
+                    __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b0[j][i], acc[T][0], 0, 0, 0);
+                acc[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[KS / 4 + i], b1[j][i],
+                                                                  acc[T][1], 0, 0, 0);
             }
 #pragma unroll
             for (int i = 0; i < KS / 2; i++)
-                acc[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b2[i], acc[T][2], 0, 0, 0);
+                acc[T][2] =
+                    __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b2[j][i], acc[T][2], 0, 0, 0);
         }
         // epilogue: lane (g, t) holds row t, columns cb .. cb + 15
         const long long cb = col0 + 16 * g;
@@ -1797,9 +1821,10 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
 #pragma unroll
         for (int T = 0; T < 4; T++)
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                y[4 * T + j] = fold(fold(((KS >= 16 ? fold(acc[T][2][j]) : acc[T][2][j]) << 8) +
-                                         acc[T][1][j] - acc[T][0][j]));
+            for (int jj = 0; jj < 4; jj++)
+                y[4 * T + jj] =
+                    fold(fold(((KS >= 16 ? fold(acc[T][2][jj]) : acc[T][2][jj]) << 8) +
+                              acc[T][1][jj] - acc[T][0][jj]));
         // restored OOR symbols of the received rows (decode_prepare,
         // src/fec_base.h:1361-1404): 65536 == -1 where the stored word is 0
         const uint32_t st0 = static_cast<uint32_t>(col0);
@@ -1816,10 +1841,10 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
                 y[c] = (trow && d == c) ? yc : y[c];
             }
         }
-        if (__builtin_amdgcn_ballot_w64(rs != 1)) {
+        if (__builtin_amdgcn_ballot_w64(rs[j] != 1)) {
 #pragma unroll
             for (int c = 0; c < 16; c++)
-                y[c] = fold(fold(mul_rs(y[c], rs)));
+                y[c] = fold(fold(mul_rs(y[c], rs[j])));
         }
         uint32_t bad = 0;
 #pragma unroll
@@ -1830,7 +1855,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             for (int c = 0; c < 16; c++) {
                 if (static_cast<uint32_t>(y[c]) > 65535u) {
                     if (rec && trow)
-                        record_oor(out_oor, s, pr[0], cb + c);
+                        record_oor(out_oor, s, pr[j][0], cb + c);
                     y[c] = 0;  // 65536 (or its alias -1) is stored as 0
                 }
             }
@@ -1853,10 +1878,11 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             const int orow = 8 * h + (l >> 3), c = l & 7;
             const qi_v4u v =
                 *reinterpret_cast<const qi_v4u*>(stg + orow * O::kStagePitch + 16 * c);
-            const int ot = 16 * rbc + orow;
-            const uint32_t vo = ot < L.R ? static_cast<uint32_t>(pr[1 + h]) * ors +
-                                               static_cast<uint32_t>((col0 + 8 * c) * 2)
-                                         : 0x80000000u;
+            const int ot = 16 * rbj[j] + orow;
+            const uint32_t vo = (act[j] && ot < L.R)
+                                    ? static_cast<uint32_t>(pr[j][1 + h]) * ors +
+                                          static_cast<uint32_t>((col0 + 8 * c) * 2)
+                                    : 0x80000000u;
             __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo), 0, kAuxStMf);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1878,8 +1904,13 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         const bool more = tile + 1 < t1;  // block-uniform
         if (more)
             issue_rows(tile + 1);
-        if (act)
-            compute(img(b), static_cast<long long>(tile) * 64, nl[b], s_i(b), s_col(b));
+        const long long col0 = static_cast<long long>(tile) * NCOL + 64 * st;
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            ((act[J] ? compute(img(b), col0, nl[b], s_i(b), s_col(b),
+                               std::integral_constant<int, J>{})
+                     : void()),
+             ...);
+        }(std::make_integer_sequence<int, RPW>{});
         if (more) {
             write_rows(img(b ^ 1));
             nl[b ^ 1] = stage_marks(tile + 1, b ^ 1);
@@ -2397,15 +2428,15 @@ static bool pipe_enabled()
 #endif
 static constexpr bool kMmOs = QI_MM_OS != 0;
 
-template <int KS>
+template <int KS, int WR, int RPW>
 static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 {
-    using O = OsTile<KS>;
-    const long long TS = wfull / 64;
+    using O = OsTile<KS, WR>;
+    const long long TS = wfull / O::kCols;
     if (TS <= 0 || TS > 0x7fffffffLL)
         return -1;
     const int RB = a.L.RB();
-    const int G = (RB + O::kWaves - 1) / O::kWaves;
+    const int G = (RB + WR * RPW - 1) / (WR * RPW);
     long long C = (512 + static_cast<long long>(S) * G - 1) / (static_cast<long long>(S) * G);
     C = std::max(1LL, std::min(C, std::max(1LL, TS / 4)));
     // the XCD map wants S * C a multiple of 8
@@ -2419,37 +2450,70 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
     if (hipGetDevice(&dev) != hipSuccess)
         return -2;
     const uint64_t bit = dev < 64 ? 1ull << dev : 0;
-    const bool two = a.src.base1 != nullptr;
-    const void* fn = two ? reinterpret_cast<const void*>(&matrix_os_kernel<KS, true>)
-                         : reinterpret_cast<const void*>(&matrix_os_kernel<KS, false>);
     if (O::kLds > 65536 && (!bit || !(attr_done.load(std::memory_order_acquire) & bit))) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&matrix_os_kernel<KS, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                static_cast<int>(O::kLds)) != hipSuccess ||
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&matrix_os_kernel<KS, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                static_cast<int>(O::kLds)) != hipSuccess)
+        if (hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, true>),
+                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(O::kLds)) !=
+                hipSuccess ||
+            hipFuncSetAttribute(
+                reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, false>),
+                hipFuncAttributeMaxDynamicSharedMemorySize,
+                static_cast<int>(O::kLds)) != hipSuccess)
             return -2;
         attr_done.fetch_or(bit, std::memory_order_release);
     }
-    (void)fn;
     a.tiles = static_cast<int>(TS);
-    if (two)
-        hipLaunchKernelGGL((matrix_os_kernel<KS, true>), dim3(static_cast<unsigned>(blocks)),
-                           dim3(O::kThreads), O::kLds, st, a, G, static_cast<int>(C),
-                           static_cast<int>(TS));
+    if (a.src.base1)
+        hipLaunchKernelGGL((matrix_os_kernel<KS, WR, RPW, true>),
+                           dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), O::kLds, st,
+                           a, G, static_cast<int>(C), static_cast<int>(TS));
     else
-        hipLaunchKernelGGL((matrix_os_kernel<KS, false>), dim3(static_cast<unsigned>(blocks)),
-                           dim3(O::kThreads), O::kLds, st, a, G, static_cast<int>(C),
-                           static_cast<int>(TS));
+        hipLaunchKernelGGL((matrix_os_kernel<KS, WR, RPW, false>),
+                           dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), O::kLds, st,
+                           a, G, static_cast<int>(C), static_cast<int>(TS));
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+#ifndef QI_OS_TALL4
+#define QI_OS_TALL4 0
+#endif
+// operand-stationary geometry by shape: (WR row-block slots, RPW row blocks
+// per wave); 0 = the per-launch kernel
+struct OsGeom {
+    int wr, rpw;
+};
+inline OsGeom os_geom(int KS, int RB)
+{
+    if (!kMmOs)
+        return {0, 0};
+    if (KS == 16 || KS == 8)
+        return {8, 1};
+    if (KS == 4) {
+        if (RB <= 4)
+            return {4, 1};
+        if (RB <= 8 || QI_OS_TALL4 == 1)
+            return {8, 1};
+        if (QI_OS_TALL4 == 4)
+            return {8, 4};
+    }
+    return {0, 0};
 }
 
 template <int KS>
 static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t st)
 {
-    if constexpr (kMmOs && (KS == 8 || KS == 16))
-        return os_launch<KS>(a, wfull, S, st);
+    if constexpr (KS == 4) {
+        const OsGeom og = os_geom(KS, a.L.RB());
+        if (og.wr == 4 && og.rpw == 1)
+            return os_launch<KS, 4, 1>(a, wfull, S, st);
+        if (og.wr == 8 && og.rpw == 1)
+            return os_launch<KS, 8, 1>(a, wfull, S, st);
+        if (og.wr == 8 && og.rpw == 4)
+            return os_launch<KS, 8, 4>(a, wfull, S, st);
+    } else if constexpr (KS == 8 || KS == 16) {
+        if (os_geom(KS, a.L.RB()).wr)
+            return os_launch<KS, 8, 1>(a, wfull, S, st);
+    }
     constexpr int NSTS = KS == 1 ? 16 : 8;
     const int RB = a.L.RB();
     if constexpr (KS == 16) {
@@ -2582,8 +2646,10 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
             nst = 4;
             rsplit = true;
         }
-        if (kMmOs && (KS == 8 || KS == 16))
-            r = "matrix_os_kernel<" + std::to_string(KS) + ">";
+        const OsGeom og = os_geom(KS, RB);
+        if (og.wr)
+            r = "matrix_os_kernel<" + std::to_string(KS) + "," + std::to_string(og.wr) + "," +
+                std::to_string(og.rpw) + ">";
         else
             r = "matrix_mfma_kernel<" + std::to_string(KS) + "," + std::to_string(nst) + "," +
                 std::to_string(nw) + "," + (rsplit ? "true" : "false") + ">";
