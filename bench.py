@@ -45,13 +45,16 @@ CONFIGS = {
     "cfg2": (16, 48, 65536, 4096),
     "cfg3": (64, 960, 4096, 1024),   # high fragmentation, n = 1024
     "cfg1": (4, 4, 1024, 100),       # the reference's CPU plumbing case
-    # larger codes: not BASELINE configs, extra lines.  64 < k <= 256 on
-    # the matrix cores, k > 256 on the NTT path
+    # larger codes: not BASELINE configs, extra lines.  64 < k <= 384 on
+    # the matrix cores (whole 1024-column tiles above 256), larger k on the
+    # NTT engine
     "k32": (32, 32, 65536, 1024),    # n = 64: the KS = 2 matrix decode
     "k128": (128, 128, 65536, 128),  # n = 256
     "k200": (200, 56, 65536, 64),    # n = 256
     "k256": (256, 768, 4096, 256),   # n = 1024
-    "k300": (300, 212, 65536, 32),   # n = 512, len_2k = 1024 (NTT engine)
+    "k300": (300, 212, 65536, 32),   # n = 512: the matrix cores at KS = 20
+    "k384": (384, 128, 65536, 32),   # n = 512: the largest matrix-path k
+    "k1000": (1000, 24, 65536, 16),  # n = 1024, len_2k = 2048: NTT engine
     # cfg3's code at 64 KiB packets (the same bytes per step as cfg3)
     "cfg3p64": (64, 960, 65536, 64),
 }

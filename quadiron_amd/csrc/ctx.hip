@@ -198,10 +198,10 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
     int by_pos, long long words, uint32_t* err)
 {
-    __shared__ uint32_t xs[256];
-    __shared__ uint32_t A[257];
-    __shared__ uint32_t cinv[256];    // 1 / A'(x_i)
-    __shared__ uint32_t aprime[256];  // A'(x_i)
+    __shared__ uint32_t xs[kMatMaxKin];
+    __shared__ uint32_t A[kMatMaxKin + 1];
+    __shared__ uint32_t cinv[kMatMaxKin];    // 1 / A'(x_i)
+    __shared__ uint32_t aprime[kMatMaxKin];  // A'(x_i)
     // k x k matrix, sized by the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
     // limited the kernel to 4 workgroups per CU
     extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
@@ -269,16 +269,17 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                 a = subm(prev, mulm(xs[i], a));
             }
         } else {
-            // slot u holds coefficient 64 u + lane (u < nslot <= 4)
+            // slot u holds coefficient 64 u + lane (u < nslot <= 6)
+            constexpr int NS = kMatMaxKin / 64;
             const int nslot = (k + 63) / 64;
-            uint32_t au[4] = {a, 0u, 0u, 0u};
+            uint32_t au[NS] = {a};
             for (int i = 0; i < k; i++) {
-                uint32_t prev[4];
+                uint32_t prev[NS];
 #pragma unroll
-                for (int u = 0; u < 4; u++)
+                for (int u = 0; u < NS; u++)
                     prev[u] = __shfl_up(au[u], 1);
 #pragma unroll
-                for (int u = 1; u < 4; u++) {
+                for (int u = 1; u < NS; u++) {
                     const uint32_t top = __shfl(au[u - 1], 63);  // 64 u - 1 -> 64 u
                     if (tid == 0)
                         prev[u] = top;
@@ -287,13 +288,13 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                     prev[0] = 0;
                 const uint32_t x = xs[i];
 #pragma unroll
-                for (int u = 0; u < 4; u++)
+                for (int u = 0; u < NS; u++)
                     if (u < nslot)
                         au[u] = subm(prev[u], mulm(x, au[u]));
             }
             a = au[0];
 #pragma unroll
-            for (int u = 1; u < 4; u++)
+            for (int u = 1; u < NS; u++)
                 if (u < nslot)
                     A[64 * u + tid] = au[u];
         }
@@ -353,8 +354,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     __syncthreads();
     {
         // LPR lanes per row: 4 entries per lane at k = 64
+        // (16 entries per lane: lpr = 32 covers k <= 512)
         const int q4 = (k + 3) / 4;
-        const int lpr = q4 <= 4 ? 4 : q4 <= 8 ? 8 : 16;
+        const int lpr = q4 <= 4 ? 4 : q4 <= 8 ? 8 : q4 <= 16 ? 16 : 32;
         for (int t = tid / lpr; !(QI_PROBE_SKIP & 8) && t < L.R; t += NT / lpr)
             pack_row_grp(Mt + t * kp, cinv, L, t, mat, tid & (lpr - 1), lpr);
     }
@@ -821,7 +823,7 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
                       long long ctx_stride, const Oor* in_oor, int slot_base,
                       int by_pos, long long words, uint32_t* err, hipStream_t st)
 {
-    if (k > 256 || S <= 0)
+    if (k > kMatMaxKin || S <= 0)
         return -3;
     Oor none{nullptr, nullptr, 0, 0};
     if (k > 128) {

@@ -130,6 +130,12 @@ struct Region {
 constexpr int kAuxLd = 2;
 constexpr int kAuxSt = 18;
 constexpr int kAuxStMf = 18;
+// matrix_os_kernel's row loads: the G row-block groups of a stripe read the
+// same tiles through their XCD's L2, so they keep the default policy
+#ifndef QI_OS_AUXLD
+#define QI_OS_AUXLD 0
+#endif
+constexpr int kAuxLdOs = QI_OS_AUXLD;
 
 // XCD-aware block -> (stripe, tile) map.  Workgroups are dispatched
 // round-robin over the 8 XCDs (block b runs on XCD b % 8), so with the plain
@@ -610,8 +616,8 @@ constexpr int kRedoCols = 64;
 
 __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_stripes)
 {
-    __shared__ uint16_t xs[256 * kRedoCols];  // [input i][column]
-    __shared__ uint32_t mk[256 * (kRedoCols / 32)];
+    __shared__ uint16_t xs[kMatMaxKin * kRedoCols];  // [input i][column]
+    __shared__ uint32_t mk[kMatMaxKin * (kRedoCols / 32)];
     __shared__ uint32_t colmk[kRedoCols / 32];
     const MatLayout L = a.L;
     const int kin = L.kin;
@@ -1604,7 +1610,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
 {
     using O = OsTile<KS, WR>;
     constexpr int KH = O::kRows, RSB = O::kPitch, RPT = O::kRpt, NCOL = O::kCols;
-    static_assert(KS == 4 || KS == 8 || KS == 16, "x64 pairs with zero halves");
+    static_assert(KS % 4 == 0, "x64 pairs with zero halves");
     extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
     const MatLayout L = a.L;
     const RowSrc src = a.src;
@@ -1719,12 +1725,12 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
 #pragma unroll
         for (int r = 0; r < RPT; r++) {
             const auto v = __builtin_amdgcn_raw_buffer_load_b64(g0.r, static_cast<int>(off0[r]),
-                                                                so, kAuxLd);
+                                                                so, kAuxLdOs);
             w[r][0] = v[0];
             w[r][1] = v[1];
             if constexpr (TWO) {
                 const auto u = __builtin_amdgcn_raw_buffer_load_b64(
-                    g1.r, static_cast<int>(off1[r]), so, kAuxLd);
+                    g1.r, static_cast<int>(off1[r]), so, kAuxLdOs);
                 w[r][0] |= u[0];
                 w[r][1] |= u[1];
             }
@@ -1789,31 +1795,37 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         qi_v4i acc[4][3];
 #pragma unroll
         for (int T = 0; T < 4; T++) {
-            qi_v4i av[KS / 2];
-#pragma unroll
-            for (int i = 0; i < KS / 2; i++) {
-                auto rd = [&](int ks) {
-                    auto* pa = (__attribute__((address_space(3))) qi_v2i*)(
-                        lds + abase + 32 * ks * RSB + T * 16);
-                    return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
-                };
-                const qi_v2i x0 = rd(2 * i), x1 = rd(2 * i + 1);
-                av[i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
-            }
             acc[T][0] = qi_v4i{0, 0, 0, 0};
             acc[T][1] = qi_v4i{kt[j], kt[j], kt[j], kt[j]};
             acc[T][2] = qi_v4i{0, 0, 0, 0};
+            // the h' half of K (pairs 0 .. KS/4-1: [a|0] and [b|a]), then the
+            // l' half ([0|b] and [b|a]): KS / 4 A pairs live at a time
 #pragma unroll
-            for (int i = 0; i < KS / 4; i++) {
-                acc[T][0] =
-                    __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b0[j][i], acc[T][0], 0, 0, 0);
-                acc[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[KS / 4 + i], b1[j][i],
-                                                                  acc[T][1], 0, 0, 0);
+            for (int hf = 0; hf < 2; hf++) {
+                qi_v4i av[KS / 4];
+#pragma unroll
+                for (int i = 0; i < KS / 4; i++) {
+                    auto rd = [&](int ks) {
+                        auto* pa = (__attribute__((address_space(3))) qi_v2i*)(
+                            lds + abase + 32 * ks * RSB + T * 16);
+                        return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
+                    };
+                    const int pi = hf * (KS / 4) + i;
+                    const qi_v2i x0 = rd(2 * pi), x1 = rd(2 * pi + 1);
+                    av[i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
+                }
+#pragma unroll
+                for (int i = 0; i < KS / 4; i++) {
+                    if (hf == 0)
+                        acc[T][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b0[j][i],
+                                                                          acc[T][0], 0, 0, 0);
+                    else
+                        acc[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b1[j][i],
+                                                                          acc[T][1], 0, 0, 0);
+                    acc[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                        av[i], b2[j][hf * (KS / 4) + i], acc[T][2], 0, 0, 0);
+                }
             }
-#pragma unroll
-            for (int i = 0; i < KS / 2; i++)
-                acc[T][2] =
-                    __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b2[j][i], acc[T][2], 0, 0, 0);
         }
         // epilogue: lane (g, t) holds row t, columns cb .. cb + 15
         const long long cb = col0 + 16 * g;
@@ -2333,7 +2345,9 @@ int matrix_kp(int kin)
         return 64;
     if (pairs <= 128)
         return 128;
-    return -1;  // k > 256 runs the NTT path (ntt.hip)
+    if (2 * pairs <= kMatMaxKin + 1)
+        return 256;  // 256 < k <= 384: matrix cores only (no dot2 tails)
+    return -1;  // larger k runs the NTT path (ntt.hip)
 }
 
 template <int KP, int COLS, bool BUF>
@@ -2486,7 +2500,7 @@ inline OsGeom os_geom(int KS, int RB)
 {
     if (!kMmOs)
         return {0, 0};
-    if (KS == 16 || KS == 8)
+    if (KS >= 8)
         return {8, 1};
     if (KS == 4) {
         if (RB <= 4)
@@ -2510,13 +2524,15 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
             return os_launch<KS, 8, 1>(a, wfull, S, st);
         if (og.wr == 8 && og.rpw == 4)
             return os_launch<KS, 8, 4>(a, wfull, S, st);
-    } else if constexpr (KS == 8 || KS == 16) {
+    } else if constexpr (KS == 8 || KS == 16 || KS == 20 || KS == 24) {
         if (os_geom(KS, a.L.RB()).wr)
             return os_launch<KS, 8, 1>(a, wfull, S, st);
     }
     constexpr int NSTS = KS == 1 ? 16 : 8;
     const int RB = a.L.RB();
-    if constexpr (KS == 16) {
+    if constexpr (KS > 16) {
+        return -1;  // only the operand-stationary kernel takes kin > 256
+    } else if constexpr (KS == 16) {
         // 128 < k <= 256: a 512-row byte-plane image of 64 columns (41 KB);
         // 8 waves over 128 columns (94 KB, 1 block per CU) measured the
         // same at k200 / k256 (profiles/r2_ab_round2b.txt)
@@ -2602,8 +2618,12 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
             rc = mfma_dispatch<4>(a, wfull, S, st);
         else if (L.KS() == 8)
             rc = mfma_dispatch<8>(a, wfull, S, st);
-        else
+        else if (L.KS() == 16)
             rc = mfma_dispatch<16>(a, wfull, S, st);
+        else if (L.KS() == 20)
+            rc = mfma_dispatch<20>(a, wfull, S, st);
+        else
+            rc = mfma_dispatch<24>(a, wfull, S, st);
         if (rc || wfull == words)
             return rc;
         a.ext.c0 = wfull;

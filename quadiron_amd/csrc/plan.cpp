@@ -164,13 +164,18 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
 
     bool ok = hipMalloc(&p->d_err, 4) == hipSuccess && hipMemset(p->d_err, 0, 4) == hipSuccess;
     if (ok && p->K > 256) {
-        // k > 256: NTT-structured encode/decode (ntt.hip), any k + m <= 65536
+        // k > 256: NTT-structured encode/decode (ntt.hip), any k + m <= 65536;
+        // up to k = 384 the matrix cores also take the whole-tile batches
+        // (qi_gpu.cpp use_matrix: words a multiple of 1024), with the
+        // generator below and per-stripe k x k contexts
         p->ntt = 1;
+        p->mbig = k <= kMatMaxKin ? 1 : 0;
         ok = ntt_plan_init(p) == 0;
-    } else if (ok) {
+    }
+    if (ok && (!p->ntt || p->mbig)) {
         // twist factors w^{v t} for the encode passes (K <= 32; K = 64 to
         // 256 encode on the matrix cores)
-        if (!p->sys && !enc_matrix(p->K)) {
+        if (!p->ntt && !p->sys && !enc_matrix(p->K)) {
             const int passes = p->n / p->K;
             std::vector<int32_t> tw(static_cast<size_t>(passes) * p->K);
             for (int v = 0; v < passes; v++)
@@ -183,7 +188,7 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
         }
         // generator matrix for the systematic encode (and the matrix-core
         // A/B knob of the non-systematic one): outputs x inputs
-        if (ok && (p->sys || enc_matrix(p->K))) {
+        if (ok && (p->sys || p->mbig || enc_matrix(p->K))) {
             const int kp = matrix_kp(k);
             MatLayout L{p->n_outputs, k, kp};
             std::vector<uint32_t> M;

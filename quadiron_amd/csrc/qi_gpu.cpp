@@ -25,13 +25,22 @@ hipStream_t st(void* s)
     return static_cast<hipStream_t>(s);
 }
 
+// the matrix path (contexts, kernels) for this batch width: every k <= 256,
+// and 256 < k <= 384 when the columns tile into whole 1024-column blocks
+// (the operand-stationary kernel has no column tail there); otherwise the
+// NTT engine
+bool use_matrix(const qi_plan* p, long long words)
+{
+    return !p->ntt || (p->mbig && words % kRouteTile == 0);
+}
+
 }  // namespace
 
 namespace qi {
 
 long long ctx_stride(const qi_plan* p, long long words)
 {
-    if (p->ntt)
+    if (!use_matrix(p, words))
         return ntt_ctx_words(p);
     const MatLayout L = ctx_layout(p);
     return static_cast<long long>(L.words()) + 2 * L.KP +
@@ -59,7 +68,7 @@ int build_ctx(qi_plan* p, const uint16_t* d_ids, int n_stripes, const Oor* in,
     if (!d_ids)
         return -1;
     const long long cs = ctx_stride(p, words);
-    if (p->ntt)
+    if (!use_matrix(p, words))
         return ntt_build_ctx(p, d_ids, n_stripes, static_cast<int32_t*>(d_ctx), cs, s);
     const MatLayout L = ctx_layout(p);
     return launch_decode_ctx(p->k, p->n, p->r, p->sys ? 1 : 0, L, d_ids, n_stripes,
@@ -92,7 +101,7 @@ int qi_gpu_encode(qi_plan* p, const uint16_t* d_data, long long dss,
         return 0;
     Oor oor{d_counts, d_entries, p->n_outputs, cap};
     RowDst out{d_out, oss, ors};
-    if (p->ntt)
+    if (!use_matrix(p, words))
         return ntt_encode(p, d_data, dss, drs, out, words, n_stripes,
                           d_counts ? &oor : nullptr, st(stream));
     if (!p->d_gen)
@@ -152,7 +161,7 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
     const long long cs = ctx_stride(p, words);
     const int32_t* ctx = static_cast<const int32_t*>(d_ctx);
     (void)d_ids;  // the context carries the ids (as dwords)
-    if (p->ntt)
+    if (!use_matrix(p, words))
         return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, p->sys ? p->k : 0, out,
                           words, n_stripes, st(stream));
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
@@ -193,7 +202,7 @@ int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
     RowDst out{d_out, oss, ors};
     const long long cs = ctx_stride(p, words);
     const int32_t* ctx = static_cast<const int32_t*>(d_ctx);
-    if (p->ntt)
+    if (!use_matrix(p, words))
         return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, 0, out, words,
                           n_stripes, st(stream));
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
@@ -208,7 +217,7 @@ const char* qi_gpu_kernels(const qi_plan* p, long long words)
     if (!p || words <= 0)
         return "";
     std::string enc, dec;
-    if (p->ntt) {
+    if (!use_matrix(p, words)) {
         enc = ntt_engine_name(p);
         dec = std::string("ntt_ctx_kernel + ") + ntt_engine_name(p);
     } else {

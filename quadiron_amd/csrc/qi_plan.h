@@ -83,6 +83,9 @@ struct qi_plan {
     // max(n, len_2k), balanced twiddle tables w^e / w^-e, and the systematic
     // encode's constant decode context
     int ntt = 0, len2k = 0, nmax = 0;
+    // 256 < k <= 384: batches whose columns tile exactly (words a multiple
+    // of 1024) run the matrix cores instead (d_gen, k x k contexts)
+    int mbig = 0;
     int32_t* d_tw[2] = {nullptr, nullptr};
     int32_t* d_ldstw = nullptr;  // per-pass twiddle tables of the LDS engine
     int32_t* d_sysctx = nullptr;

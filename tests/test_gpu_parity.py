@@ -242,6 +242,14 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
     (256, 768, 0, 1, 2048),
     (129, 127, 1, 1, 1100),
     (130, 900, 1, 1, 300),
+    # 256 < k <= 384 with whole 1024-column tiles: the operand-stationary
+    # matrix kernel at KS = 20 / 24 (k x k contexts, the generator encode)
+    (300, 212, 0, 2, 1024),
+    (257, 255, 0, 1, 2048),
+    (320, 100, 1, 2, 1024),   # systematic: generator + mode-1 contexts
+    (321, 63, 0, 2, 1024),    # KS = 24
+    (384, 128, 0, 1, 2048),   # largest matrix-path k
+    (384, 100, 1, 1, 1024),
     # k > 256: the NTT-structured general path (ntt.hip)
     (257, 255, 0, 1, 300),    # smallest NTT-path code
     (300, 100, 1, 1, 300),    # systematic: interpolation + NTT_n encode
@@ -463,8 +471,11 @@ def test_dense_tile_over_scratch_decodes(k, m):
     # (KP = 128, 256-column tiles) past the last whole 1024-column tile
     (200, 56, 5, [(0, 768), (2048, 2348)], 2348),
     (256, 768, 5, [(64, 832)], 2048),
-    # k > 256: the NTT engine walks the buckets itself (no tile list)
+    # 256 < k <= 384, whole tiles: the operand-stationary kernel at KS = 20
     (300, 100, 5, [(0, 768)], 1024),
+    # k > 256, ragged width: the NTT engine walks the buckets itself (no
+    # tile list)
+    (300, 100, 5, [(0, 768)], 1000),
 ])
 def test_dense_tiles_spread_decode(k, m, per_col, ranges, P):
     """Several OOR marks in every column of many tiles (crafted by solving

@@ -54,7 +54,7 @@ def roles(path):
             continue
         if not started:
             continue
-        if "ctx_kernel" in name:
+        if "ctx_kernel" in name or "ctx_lds_kernel" in name:
             phase = "decode"
         cur[phase].update(ctr)
         cur[phase]["dispatches"] += 1
