@@ -130,12 +130,10 @@ struct Region {
 constexpr int kAuxLd = 2;
 constexpr int kAuxSt = 18;
 constexpr int kAuxStMf = 18;
-// matrix_os_kernel's row loads: the G row-block groups of a stripe read the
-// same tiles through their XCD's L2, so they keep the default policy
-#ifndef QI_OS_AUXLD
-#define QI_OS_AUXLD 0
-#endif
-constexpr int kAuxLdOs = QI_OS_AUXLD;
+// matrix_os_kernel's row loads: default policy (its G row-block groups read
+// the same tiles through their XCD's L2; nt measured the same at k200 /
+// k256 / cfg3, gpurun_out ab_aux)
+constexpr int kAuxLdOs = 0;
 
 // XCD-aware block -> (stripe, tile) map.  Workgroups are dispatched
 // round-robin over the 8 XCDs (block b runs on XCD b % 8), so with the plain
@@ -284,10 +282,8 @@ __device__ __forceinline__ void st(const Region<BUF>& g, uint32_t row,
 // one OR-reduction per pass and fixed up off the fast path.
 // KEQ: k == K (no zero-padded inputs to mask).
 // ---------------------------------------------------------------------------
-#ifndef QI_ENC_PAIR
-#define QI_ENC_PAIR 1
-#endif
-static constexpr bool kEncPair = QI_ENC_PAIR != 0;
+// cfg2 encode passes in store-interleaved pairs (3.675 -> 3.627 ms)
+static constexpr bool kEncPair = true;
 
 template <int K, int COLS, bool FULL, bool KEQ, bool BUF>
 __device__ __forceinline__ void encode_body(
@@ -1045,10 +1041,10 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(MatArgs a)
 // matrix_kernel.
 // ---------------------------------------------------------------------------
 typedef int qi_v4i __attribute__((ext_vector_type(4)));
-#ifndef QI_MM_PIPE
-#define QI_MM_PIPE 1
-#endif
-static constexpr bool kMmPipe = QI_MM_PIPE != 0;
+// the KS = 4 super-tile loop in pairs, the next tile's MFMAs interleaved
+// with this one's epilogue (cfg3 encode 1.078 -> 1.063 ms; at KS = 2 the
+// second accumulator set cost occupancy: k32 decode 0.83 -> 0.99 ms)
+static constexpr bool kMmPipe = true;
 typedef int qi_v2i __attribute__((ext_vector_type(2)));
 typedef unsigned int qi_v4u __attribute__((ext_vector_type(4)));
 
@@ -1931,300 +1927,6 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     }
 }
 
-// ---------------------------------------------------------------------------
-// Pipelined persistent matrix-core kernel for short matrices (R <= 64 rows,
-// 16 < kin <= 64: the decodes of 17 <= k <= 64, e.g. BASELINE cfg3).
-//
-// The per-launch kernel above stages a 512-column tile (68 KB of image),
-// computes it, and exits: with two blocks per CU, every block's row loads
-// (and its preamble: ids, route table, operand tiles) sit on the critical
-// path.  Here a grid of (blocks per CU x CUs) blocks walks contiguous
-// ranges of 256-column tiles; while a tile is on the matrix cores, the
-// block's next tile is already in flight into registers (16 b64 row loads
-// per thread), and the operand tiles stay in registers while the stripe
-// does.  46 KB of LDS per block: 3 blocks (12 waves) per CU.
-// Per tile: wait for the rows -> barrier -> byte-plane image + marks ->
-// barrier -> issue the next tile's rows -> MFMAs, epilogue, stores.
-// Wave w takes row block w % nrb over super tiles [(w / nrb) nrb, +nrb)
-// (nrb = RB, 3 -> 4): every wave issues the same MFMA count.
-// ---------------------------------------------------------------------------
-template <int KS>
-struct PipeTile {
-    static constexpr int kThreads = 256;
-    static constexpr int kCols = 256;          // columns per tile
-    static constexpr int kRows = 16 * KS;      // rows per byte plane (KH)
-    static constexpr int kPitch = kCols + 16;  // LDS row pitch: +4 banks/row
-    static constexpr size_t kImg = static_cast<size_t>(2 * kRows) * kPitch;
-    static constexpr int kStagePitch = 144;
-    static constexpr size_t kStage = 16 * kStagePitch;
-    static constexpr size_t kMarks = kImg + 4 * kStage;
-    static constexpr size_t kLds = kMarks + 2 * 4 * kMaxTileOor + 16;
-    static constexpr int kRpt = kRows / 4;  // rows per thread (row group = wave)
-};
-
-#ifndef QI_PIPE_WAVES
-#define QI_PIPE_WAVES 2
-#endif
-template <int KS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QI_PIPE_WAVES))) void
-matrix_pipe_kernel(MatArgs a, long long n_tiles, int tps)
-{
-    using G = PipeTile<KS>;
-    constexpr int KH = G::kRows, RSB = G::kPitch, RPT = G::kRpt;
-    extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
-    uint8_t* img = qi_lds;
-    int* s_i = reinterpret_cast<int*>(qi_lds + G::kMarks);
-    uint32_t* s_col = reinterpret_cast<uint32_t*>(s_i + kMaxTileOor);
-    int* s_cnt = reinterpret_cast<int*>(s_col + kMaxTileOor);
-    const MatLayout L = a.L;
-    const RowSrc src = a.src;
-    const RowDst dst = a.dst;
-    const MatExt ext = a.ext;
-    const Oor in_oor = a.in_oor;
-    const Oor out_oor = a.out_oor;
-    const int kin = L.kin;
-    const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-    const int g = l >> 4, q = (l & 15) >> 1, p = l & 1, tl = l & 15;
-    const int RB = L.RB();
-    const int nrb = RB == 3 ? 4 : RB;
-    const int rb = wv % nrb, st0 = (wv / nrb) * nrb;
-    const long long t_begin = static_cast<long long>(blockIdx.x) * n_tiles / gridDim.x;
-    const long long t_end = static_cast<long long>(blockIdx.x + 1) * n_tiles / gridDim.x;
-    if (t_begin >= t_end)
-        return;  // block-uniform
-    const bool rec = out_oor.counts != nullptr;
-    const uint32_t ors = static_cast<uint32_t>(dst.rs * 2);
-    const uint32_t rsb0 = static_cast<uint32_t>(src.rs0 * 2);
-    const uint32_t cl = static_cast<uint32_t>(l) * 4;  // staging columns of this lane
-    const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) + 4 * ((cl % 64) / 16) + cl % 4;
-    auto* lds = (__attribute__((address_space(3))) uint8_t*)img;
-    const uint32_t abase = static_cast<uint32_t>((8 * g + q) * RSB + 8 * p);
-    uint8_t* stg = qi_lds + G::kImg + wv * G::kStage;
-
-    // rows of tile t: this thread's 4 columns of rows wv, wv + 4, ...
-    uint32_t w[RPT][2];
-    auto issue_rows = [&](long long t) {
-        const int s = static_cast<int>(t / tps);
-        const long long col0 = (t - static_cast<long long>(s) * tps) * G::kCols;
-        const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
-        int idv[RPT];
-        if (sid && !src.by_pos) {
-#pragma unroll
-            for (int r = 0; r < RPT; r++) {
-                const int i = 4 * r + wv;
-                idv[r] = sid[i < kin ? i : kin - 1];
-            }
-        } else {
-#pragma unroll
-            for (int r = 0; r < RPT; r++) {
-                const int i = 4 * r + wv;
-                idv[r] = i < kin ? i : kin - 1;
-            }
-        }
-        const uint32_t voff = static_cast<uint32_t>((col0 + cl) * 2);
-        const Region<true> g0(src.base0 + s * src.ss0, ext.e0);
-        if (!src.base1) {
-#pragma unroll
-            for (int r = 0; r < RPT; r++)
-                ld_dw<2, true, kAuxLd>(g0, static_cast<uint32_t>(idv[r]) * rsb0, voff, w[r]);
-        } else {
-            const Region<true> g1(src.base1 + s * src.ss1, ext.e1);
-#pragma unroll
-            for (int r = 0; r < RPT; r++) {
-                const int id = idv[r];
-                const bool lo = id < src.split;
-                Region<true> gg = g0;
-                gg.r = lo ? g0.r : g1.r;
-                const uint32_t off = static_cast<uint32_t>(
-                    lo ? id * src.rs0 * 2 : (id - src.split) * src.rs1 * 2);
-                ld_dw<2, true, kAuxLd>(gg, off, voff, w[r]);
-            }
-        }
-    };
-
-    // the stripe's operand tiles of row block rb, kmf / row scale / output
-    // rows of this lane (reloaded when the stripe changes)
-    qi_v2i bop[KS][3];
-    int32_t kt = 0, rs = 1, pr[3] = {0, 0, 0};
-    int cur = -1;
-    auto load_ops = [&](int s) {
-        const int32_t* M = a.mat + s * a.ms;
-        const int32_t* mf = M + L.mf();
-#pragma unroll
-        for (int ks = 0; ks < KS; ks++)
-#pragma unroll
-            for (int ty = 0; ty < 3; ty++)
-                bop[ks][ty] = *reinterpret_cast<const qi_v2i*>(
-                    mf + ((rb * KS + ks) * 3 + ty) * 128 + l * 2);
-        const int t = 16 * rb + tl, tc = t < L.R ? t : L.R - 1;
-        const int32_t k0 = M[L.kmf() + tc], r0 = M[L.rscale_mf() + tc];
-        kt = t < L.R ? k0 : 0;
-        rs = t < L.R ? r0 : 1;
-        pr[0] = a.rowmap[tc];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int ot = 16 * rb + 8 * h + (l >> 3);
-            pr[1 + h] = a.rowmap[ot < L.R ? ot : L.R - 1];
-        }
-    };
-
-    issue_rows(t_begin);
-    for (long long t = t_begin; t < t_end; t++) {
-        const int s = static_cast<int>(t / tps);
-        const long long col0 = (t - static_cast<long long>(s) * tps) * G::kCols;
-        if (s != cur) {  // block-uniform
-            load_ops(s);
-            cur = s;
-        }
-        const int32_t* M = a.mat + s * a.ms;
-        const int32_t* plain = M + L.plain();
-        // marks of the received rows in this tile: the route table, or a
-        // bucket scan when it overflowed (or is absent)
-        int n_rm = 0;
-        const uint32_t* rm = nullptr;
-        bool scan = in_oor.counts != nullptr;
-        if (a.route && scan) {
-            const uint32_t* rt = a.route + s * a.rstride + (col0 / kRouteTile) * kRouteStride;
-            const uint32_t rc = rt[0];
-            if (rc <= static_cast<uint32_t>(kRouteCap)) {
-                n_rm = static_cast<int>(rc);
-                rm = rt + 1;
-                scan = false;
-            }
-        }
-        __syncthreads();  // the previous tile's image, marks and staging are free
-#pragma unroll
-        for (int r = 0; r < RPT; r++) {
-            const int i = 4 * r + wv;
-            const uint32_t hi = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x07050301u) ^ 0x80808080u;
-            const uint32_t lo = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x06040200u) ^ 0x80808080u;
-            *reinterpret_cast<uint32_t*>(img + i * RSB + lpos) = hi;
-            *reinterpret_cast<uint32_t*>(img + (KH + i) * RSB + lpos) = lo;
-        }
-        int n_lm = 0;
-        bool slow = false;
-        if (scan) {  // block-uniform; its barriers also publish the image
-            const OorScan sc{in_oor, a.ids ? a.ids + s * a.is : nullptr, src.by_pos,
-                             a.slot_base, kin, s, false};
-            const int cnt = scan_tile_marks(sc, col0, col0 + G::kCols, a.words, s_cnt, s_i,
-                                            s_col, a.err);
-            slow = cnt > kMaxTileOor;
-            n_lm = min(cnt, kMaxTileOor);
-        } else {
-            stage_route_marks(rm, n_rm, col0, s_i, s_col);
-            __syncthreads();
-            n_lm = n_rm;
-        }
-        // the next tile's rows fly while this one is on the matrix cores
-        if (t + 1 < t_end)
-            issue_rows(t + 1);
-
-        const int trow = 16 * rb + tl;
-        const bool live = trow < L.R;
-        const int tcl = live ? trow : L.R - 1;
-        const Region<true> go(dst.base + s * dst.ss, ext.eo);
-#pragma unroll 1
-        for (int st = st0; st < st0 + nrb; st++) {
-            qi_v4i acc[4][3];
-#pragma unroll
-            for (int T = 0; T < 4; T++) {
-                acc[T][0] = qi_v4i{0, 0, 0, 0};
-                acc[T][1] = qi_v4i{kt, kt, kt, kt};
-                acc[T][2] = qi_v4i{0, 0, 0, 0};
-                auto rd_a = [&](int ks) {
-                    auto* pa = (__attribute__((address_space(3))) qi_v2i*)(
-                        lds + abase + 32 * ks * RSB + (4 * st + T) * 16);
-                    return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
-                };
-#pragma unroll
-                for (int ks = 0; ks < KS; ks += 2) {
-                    const qi_v2i a0 = rd_a(ks), a1 = rd_a(ks + 1);
-                    const qi_v4i av{a0.x, a0.y, a1.x, a1.y};
-#pragma unroll
-                    for (int ty = 0; ty < 3; ty++) {
-                        if ((ty == 0 && ks >= KS / 2) || (ty == 1 && ks + 1 < KS / 2))
-                            continue;
-                        const qi_v4i b{bop[ks][ty].x, bop[ks][ty].y, bop[ks + 1][ty].x,
-                                       bop[ks + 1][ty].y};
-                        acc[T][ty] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, b, acc[T][ty],
-                                                                           0, 0, 0);
-                    }
-                }
-            }
-            // epilogue: lane (g, t) holds row t, columns cb .. cb + 15
-            const long long cb = col0 + 64 * st + 16 * g;
-            int32_t y[16];
-#pragma unroll
-            for (int T = 0; T < 4; T++)
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    y[4 * T + j] = fold(fold((acc[T][2][j] << 8) + acc[T][1][j] - acc[T][0][j]));
-            // restored OOR symbols (decode_prepare): see matrix_mfma_kernel
-            const uint32_t stc = static_cast<uint32_t>(col0 + 64 * st);
-            for (int e = 0; e < n_lm; e++) {
-                const uint32_t wcu = __builtin_amdgcn_readfirstlane(s_col[e]);
-                if (wcu - stc >= 64u)
-                    continue;
-                const int pos = __builtin_amdgcn_readfirstlane(s_i[e]);
-                const long long d = static_cast<long long>(wcu) - cb;
-                const int32_t corr = plain[tcl * kin + pos];
-#pragma unroll
-                for (int c = 0; c < 16; c++) {
-                    const int32_t yc = fold(fold(y[c] - corr));
-                    y[c] = (live && d == c) ? yc : y[c];
-                }
-            }
-            if (__builtin_amdgcn_ballot_w64(rs != 1)) {
-#pragma unroll
-                for (int c = 0; c < 16; c++)
-                    y[c] = fold(fold(mul_rs(y[c], rs)));
-            }
-            uint32_t bad = 0;
-#pragma unroll
-            for (int c = 0; c < 16; c++)
-                bad |= static_cast<uint32_t>(y[c]);
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64((bad >> 16) != 0) != 0, 0)) {
-#pragma unroll
-                for (int c = 0; c < 16; c++) {
-                    if (static_cast<uint32_t>(y[c]) > 65535u) {
-                        if (rec && live)
-                            record_oor(out_oor, s, pr[0], cb + c);
-                        y[c] = 0;
-                    }
-                }
-            }
-            qi_v4u o0, o1;
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                o0[c] = pack_lo(static_cast<uint32_t>(y[2 * c]), static_cast<uint32_t>(y[2 * c + 1]));
-                o1[c] = pack_lo(static_cast<uint32_t>(y[8 + 2 * c]),
-                                static_cast<uint32_t>(y[8 + 2 * c + 1]));
-            }
-            // transpose through the wave's staging tile: whole 128-byte lines
-            *reinterpret_cast<qi_v4u*>(stg + tl * G::kStagePitch + 32 * g) = o0;
-            *reinterpret_cast<qi_v4u*>(stg + tl * G::kStagePitch + 32 * g + 16) = o1;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int orow = 8 * h + (l >> 3), c = l & 7;
-                const qi_v4u v =
-                    *reinterpret_cast<const qi_v4u*>(stg + orow * G::kStagePitch + 16 * c);
-                const int ot = 16 * rb + orow;
-                const uint32_t vo =
-                    ot < L.R ? static_cast<uint32_t>(pr[1 + h]) * ors +
-                                   static_cast<uint32_t>((col0 + 64 * st + 8 * c) * 2)
-                             : 0x80000000u;
-                __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo), 0, kAuxStMf);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (slow && tid == 0)  // rare: see matrix_redo_kernel
-            push_slow_tile(a.slow, s, col0, G::kCols);
-    }
-}
 
 // ---------------------------------------------------------------------------
 // launchers
@@ -2419,28 +2121,10 @@ static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 //    4 waves per SIMD instead of 2) measured slower on the 1024 x 64 cfg3
 //    generator (1.37 vs 1.22 ms, gpurun_out r2f), so the block stays at 4
 //    waves.
-// A/B knob (temporary): QI_MATK=1 runs the pipelined kernel instead of the
-// per-launch one (cfg3 decode 0.206 vs 0.179 ms, gpurun_out r3m2; 256-column
-// blocks of the per-launch kernel: 0.186 ms, encode 1.21 vs 1.07 ms)
-static int matk_mode()
-{
-    static const int m = [] {
-        const char* e = std::getenv("QI_MATK");
-        return e ? e[0] - '0' : 0;
-    }();
-    return m;
-}
-static bool pipe_enabled()
-{
-    return matk_mode() == 1;
-}
 
 // operand-stationary kernel (KS = 8, 16): G row-block groups of 8 waves, C
 // column ranges per stripe; about two blocks per CU over the launch
-#ifndef QI_MM_OS
-#define QI_MM_OS 1
-#endif
-static constexpr bool kMmOs = QI_MM_OS != 0;
+static constexpr bool kMmOs = true;
 
 template <int KS, int WR, int RPW>
 static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
@@ -2488,9 +2172,6 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-#ifndef QI_OS_TALL4
-#define QI_OS_TALL4 0
-#endif
 // operand-stationary geometry by shape: (WR row-block slots, RPW row blocks
 // per wave); 0 = the per-launch kernel
 struct OsGeom {
@@ -2502,14 +2183,12 @@ inline OsGeom os_geom(int KS, int RB)
         return {0, 0};
     if (KS >= 8)
         return {8, 1};
-    if (KS == 4) {
-        if (RB <= 4)
-            return {4, 1};
-        if (RB <= 8 || QI_OS_TALL4 == 1)
-            return {8, 1};
-        if (QI_OS_TALL4 == 4)
-            return {8, 4};
-    }
+    // KS = 4: the short decode matrices (2 super tiles per 128-column tile)
+    // and up to 8 row blocks; the tall generators (RB = 64 at cfg3) stay on
+    // matrix_mfma_kernel (os at 1 or 4 row blocks per wave: 1.48 / 1.37 vs
+    // 1.05 ms, gpurun_out ab_os2 / ab_os3)
+    if (KS == 4 && RB <= 8)
+        return RB <= 4 ? OsGeom{4, 1} : OsGeom{8, 1};
     return {0, 0};
 }
 
@@ -2522,8 +2201,6 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
             return os_launch<KS, 4, 1>(a, wfull, S, st);
         if (og.wr == 8 && og.rpw == 1)
             return os_launch<KS, 8, 1>(a, wfull, S, st);
-        if (og.wr == 8 && og.rpw == 4)
-            return os_launch<KS, 8, 4>(a, wfull, S, st);
     } else if constexpr (KS == 8 || KS == 16 || KS == 20 || KS == 24) {
         if (os_geom(KS, a.L.RB()).wr)
             return os_launch<KS, 8, 1>(a, wfull, S, st);
@@ -2552,37 +2229,6 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
     }
 }
 
-// grid of the pipelined kernel: as many blocks as fit the chip at once
-template <int KS>
-static int pipe_launch(MatArgs a, long long wfull, int S, hipStream_t st)
-{
-    using G = PipeTile<KS>;
-    static std::atomic<int> grid_cache[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev >= 64)
-        return -2;
-    int grid = grid_cache[dev].load(std::memory_order_relaxed);
-    if (grid == 0) {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu, reinterpret_cast<const void*>(&matrix_pipe_kernel<KS>), G::kThreads,
-                G::kLds) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                hipSuccess)
-            return -2;
-        grid = (per_cu > 0 ? per_cu : 1) * cus;
-        grid_cache[dev].store(grid, std::memory_order_relaxed);
-    }
-    const int tps = static_cast<int>(wfull / G::kCols);
-    const long long n_tiles = static_cast<long long>(tps) * S;
-    if (tps <= 0)
-        return -1;
-    a.tiles = tps;
-    const long long blocks = n_tiles < grid ? n_tiles : grid;
-    hipLaunchKernelGGL((matrix_pipe_kernel<KS>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(G::kThreads), G::kLds, st, a, n_tiles, tps);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
 
 static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
 {
@@ -2608,10 +2254,6 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
         int rc;
         if (L.KS() == 1)
             rc = mfma_dispatch<1>(a, wfull, S, st);
-        else if (L.KS() == 2 && L.RB() <= 4 && pipe_enabled())
-            rc = pipe_launch<2>(a, wfull, S, st);
-        else if (L.KS() == 4 && L.RB() <= 4 && pipe_enabled())
-            rc = pipe_launch<4>(a, wfull, S, st);
         else if (L.KS() == 2)
             rc = mfma_dispatch<2>(a, wfull, S, st);
         else if (L.KS() == 4)

@@ -237,6 +237,11 @@ def main():
     gen_blocks(ref, ora, "blk_k260_m3000_sys", 260, 3000, 1, 128, 256, 40, 2, 8, out)
     gen_blocks(ref, ora, "blk_k1100_m100", 1100, 100, 0, 64, 256 + 6, 41, 2, 8, out)
     gen_blocks(ref, ora, "blk_k300_m16000", 300, 16000, 0, 32, 64 + 2, 42, 1, 8, out)
+    # 256 < k <= 384 at whole 1024-word tiles: the matrix cores at KS = 20 /
+    # 24 (round 3; ragged widths of these codes stay on the NTT engine)
+    gen_blocks(ref, ora, "blk_k300_m212_w1024", 300, 212, 0, 256, 2048, 43, 2, 8, out)
+    gen_blocks(ref, ora, "blk_k384_m128_sys_w1024", 384, 128, 1, 512, 2048, 44, 2, 8,
+               out)
 
 
 if __name__ == "__main__":
