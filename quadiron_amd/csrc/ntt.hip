@@ -1,9 +1,11 @@
-// General-k RS-FNT path (k > 256): NTT-structured encode and decode.
+// General-k RS-FNT path (k > 384, and 256 < k <= 384 at column counts that
+// are not a multiple of 1024): NTT-structured encode and decode.
 //
-// Codes with k > 256 do not fit the register codelets of encode_fnt_kernel
-// (K = ceil2(k) <= 64) nor the k x k interpolation matrices of the matrix
-// kernels (k <= 256, whose byte-split products stay exact up to there).
-// They run the reference's own algorithm as column-batched NTTs:
+// These codes do not fit the register codelets of encode_fnt_kernel
+// (K = ceil2(k) <= 64) nor the matrix kernels (the operand-stationary
+// kernel's LDS image tops out at k = 384, and it has no column tail above
+// k = 256: qi_gpu.cpp use_matrix).  They run the reference's own algorithm
+// as column-batched NTTs:
 //
 //   non-systematic encode  NTT_n of the k data rows zero-padded to n
 //                          (Radix2::fft, src/fft_2n.h:360-407; outputs

@@ -79,7 +79,7 @@ struct qi_plan {
     // identity map of the k x k decode matrices
     int32_t* d_rowmap = nullptr;
     int32_t* d_rowid = nullptr;
-    // general-k path (k > 256, ntt.hip): transforms of length <= nmax =
+    // general-k path (k > 256, ntt.hip; see mbig): transforms of length <= nmax =
     // max(n, len_2k), balanced twiddle tables w^e / w^-e, and the systematic
     // encode's constant decode context
     int ntt = 0, len2k = 0, nmax = 0;
