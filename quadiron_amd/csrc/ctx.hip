@@ -76,6 +76,46 @@ __device__ __forceinline__ uint32_t powm(uint32_t b, uint32_t e)
     return r;
 }
 
+// x * y mod q for |x|, |y| < 2^17: the 48-bit product as v_mul_i32_i24 +
+// v_mul_hi_i32_i24, reduced with 2^32 = 1 and 2^16 = -1: |result| < 65600
+__device__ __forceinline__ int32_t mul_lz(int32_t x, int32_t y)
+{
+    uint32_t lo;
+    int32_t hi;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(lo) : "v"(x), "v"(y));
+    asm("v_mul_hi_i32_i24 %0, %1, %2" : "=v"(hi) : "v"(x), "v"(y));
+    return static_cast<int32_t>(lo & 0xffffu) - static_cast<int32_t>(lo >> 16) + hi;
+}
+
+// canonical residue of |y| < 98305 (fold -> [-2, 65537], then +-q)
+__device__ __forceinline__ uint32_t canon_lz(int32_t y)
+{
+    const int32_t f = fold(y);
+    const int32_t c = f < 0 ? f + 65537 : f;
+    return static_cast<uint32_t>(c >= 65537 ? c - 65537 : c);
+}
+
+// x^(2^16 - 1) = x^-1 (x != 0) by the chain x^(2^2-1), x^(2^4-1),
+// x^(2^8-1), x^(2^16-1): 15 squarings + 4 multiplies, all lazy
+__device__ __forceinline__ uint32_t inv_lz(uint32_t xc)
+{
+    const int32_t x = balanced(xc);
+    const int32_t e2 = mul_lz(mul_lz(x, x), x);        // x^3
+    int32_t t = mul_lz(e2, e2);
+    t = mul_lz(t, t);                                  // x^12
+    const int32_t e4 = mul_lz(t, e2);                  // x^15
+    t = e4;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        t = mul_lz(t, t);
+    const int32_t e8 = mul_lz(t, e4);                  // x^255
+    t = e8;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        t = mul_lz(t, t);
+    return canon_lz(mul_lz(t, e8));                    // x^65535
+}
+
 // NT threads: the Lagrange part runs on the first wave (lane = point); the
 // row packing and the MFMA operand tiles use every thread (NT = 256 for
 // k > 32, where they dominate and there are few stripes per launch).
@@ -211,6 +251,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // instruction at k = 64)
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
+    QI_TS(0);
     int32_t* mat = ctx + s * ctx_stride;
     // BIG (128 < k <= 256): the k x k matrix (up to 256 KB) does not fit
     // LDS; its rows live in the context's own `plain` section (pitch k),
@@ -256,71 +297,81 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             }
         }
     }
-    // A(x) = prod_i (x - x_i), lane d holding coefficient d (and d + 64,
-    // d + 128, ... for k > 64).  A is monic: A[k] = 1 is set explicitly, so
-    // k = 64 (128, 256) needs no 65th (129th, 257th) coefficient slot.
+    QI_TS(1);
+    // A(x) = prod_i (x - x_i) on wave 0: slot u of lane d holds coefficient
+    // 64 u + d (u < nslot <= 6), lazy (folded once per step, |a| < 2^17):
+    // the shift by DPP (wave_shr:1) with the slot carry by readlane, the
+    // product as mul_lz, x_i by readlane from the lane-held points (the
+    // ds_bpermute shifts and canonical mulm of round 2 took ~620 cycles per
+    // step: 62 us of a k = 200 context).  A is monic: A[k] = 1 is set
+    // explicitly, so k = 64 u needs no extra slot.  Stored balanced.
     if (!(QI_PROBE_SKIP & 2) && tid < 64) {  // wave 0 (wave-uniform)
-        uint32_t a = tid == 0 ? 1u : 0u;
-        if (k <= 64) {
-            for (int i = 0; i < k; i++) {
-                uint32_t prev = __shfl_up(a, 1);
-                if (tid == 0)
-                    prev = 0;
-                a = subm(prev, mulm(xs[i], a));
-            }
-        } else {
-            // slot u holds coefficient 64 u + lane (u < nslot <= 6)
-            constexpr int NS = kMatMaxKin / 64;
-            const int nslot = (k + 63) / 64;
-            uint32_t au[NS] = {a};
-            for (int i = 0; i < k; i++) {
-                uint32_t prev[NS];
+        constexpr int NS = kMatMaxKin / 64;
+        const int nslot = (k + 63) / 64;
+        int32_t xv[NS], au[NS];
 #pragma unroll
-                for (int u = 0; u < NS; u++)
-                    prev[u] = __shfl_up(au[u], 1);
-#pragma unroll
-                for (int u = 1; u < NS; u++) {
-                    const uint32_t top = __shfl(au[u - 1], 63);  // 64 u - 1 -> 64 u
-                    if (tid == 0)
-                        prev[u] = top;
-                }
-                if (tid == 0)
-                    prev[0] = 0;
-                const uint32_t x = xs[i];
-#pragma unroll
-                for (int u = 0; u < NS; u++)
-                    if (u < nslot)
-                        au[u] = subm(prev[u], mulm(x, au[u]));
-            }
-            a = au[0];
-#pragma unroll
-            for (int u = 1; u < NS; u++)
-                if (u < nslot)
-                    A[64 * u + tid] = au[u];
+        for (int u = 0; u < NS; u++) {
+            const int i = 64 * u + tid;
+            xv[u] = i < k ? balanced(xs[i]) : 0;
+            au[u] = (u == 0 && tid == 0) ? 1 : 0;
         }
-        A[tid] = a;
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            if (u >= nslot)
+                break;
+            const int cnt = min(64, k - 64 * u);
+            for (int i0 = 0; i0 < cnt; i0++) {
+                const int32_t x = __builtin_amdgcn_readlane(xv[u], i0);
+                int32_t prev[NS];
+#pragma unroll
+                for (int v = 0; v < NS; v++) {
+                    if (v >= nslot)
+                        break;
+                    prev[v] = __builtin_amdgcn_update_dpp(0, au[v], 0x138, 0xf, 0xf, false);
+                    if (v > 0) {
+                        const int32_t top = __builtin_amdgcn_readlane(au[v - 1], 63);
+                        prev[v] = tid == 0 ? top : prev[v];
+                    }
+                }
+#pragma unroll
+                for (int v = 0; v < NS; v++) {
+                    if (v >= nslot)
+                        break;
+                    au[v] = fold(prev[v] - mul_lz(au[v], x));
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NS; u++) {
+            const int i = 64 * u + tid;
+            if (u < nslot && i < k)
+                A[i] = static_cast<uint32_t>(balanced(canon_lz(au[u])));
+        }
         if (tid == 0)
             A[k] = 1;
     }
     __syncthreads();
+    QI_TS(2);
     if (!(QI_PROBE_SKIP & 4) && tid < k) {
         // Q_i = A / (x - x_i) by synthetic division from the top, and
-        // A'(x_i) = Q_i(x_i) by Horner over the same coefficients (two
-        // interleaved chains; the product prod_{j != i} (x_i - x_j) was a
-        // third serial chain).  The rows hold the unscaled values; the
-        // column scale 1 / A'(x_i) is applied by the packing pass.
-        const uint32_t xi = xs[tid];
-        uint32_t q = 1, h = 1;  // A[k]; Q_i(x_i) so far
+        // A'(x_i) = Q_i(x_i) by Horner beside it (two interleaved chains),
+        // lazy as in decode_ctx_lds_kernel (|q| < 98400, |h| < 2^18); the
+        // rows get canonical q (off the chain).  The column scale
+        // 1 / A'(x_i) is applied by the packing pass.
+        const int32_t xi = balanced(xs[tid]);
+        const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
+        int32_t q = 1, h = 1;  // A[k]; Q_i(x_i) so far
         if (mode == 0)
             Mt[(k - 1) * kp + tid] = 1;
         for (int j = k - 1; j >= 1; j--) {
-            q = addm(A[j], mulm(xi, q));
+            q = Ab[j] + mul_lz(q, xi);
             if (mode == 0)
-                Mt[(j - 1) * kp + tid] = q;
-            h = addm(mulm(h, xi), q);
+                Mt[(j - 1) * kp + tid] = canon_lz(q);
+            h = q + mul_lz(h, xi);
         }
-        aprime[tid] = h;
-        cinv[tid] = powm(h, 65535u);
+        const uint32_t ap = canon_lz(fold(h));
+        aprime[tid] = ap;
+        cinv[tid] = inv_lz(ap);
     }
     if (mode != 0) {
         // systematic: M[t][i] = Q_i(r^t) / A'(x_i), one thread per row t,
@@ -333,9 +384,13 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         if (tid < k) {
             uint32_t* row = Mt + tid * kp;
             const uint32_t et = powm(r, static_cast<uint32_t>(tid));
-            uint32_t av = 1;  // A(r^t), A monic
+            // A(r^t) by a lazy Horner chain over the balanced A (A monic)
+            const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
+            const int32_t eb = balanced(et);
+            int32_t al = 1;
             for (int j = k - 1; j >= 0; j--)
-                av = addm(mulm(av, et), A[j]);
+                al = Ab[j] + mul_lz(al, eb);
+            const uint32_t av = canon_lz(fold(al));
             uint32_t pre = 1;
             for (int i = 0; i < k; i++) {
                 const uint32_t d = subm(et, xs[i]);
@@ -352,6 +407,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         }
     }
     __syncthreads();
+    QI_TS(3);
     {
         // LPR lanes per row: 4 entries per lane at k = 64
         // (16 entries per lane: lpr = 32 covers k <= 512)
@@ -363,6 +419,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     if (!(QI_PROBE_SKIP & 16) && L.KS()) {
         // the matrix-core operand tiles, from the row-scaled entries in LDS
         __syncthreads();
+        QI_TS(4);
         // per (row t, 4 consecutive entries): split once, then place the
         // a / b byte words in their tile dwords (pack_mf_dword's layout;
         // rows t >= R are zero).  Items run row-fastest, so 16 lanes read
@@ -433,6 +490,10 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             }
         }
     }
+#ifdef QI_PROBE_TS
+    __syncthreads();
+#endif
+    QI_TS(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -451,46 +512,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
 // (shuffle reductions per row group) and 14 in the A(x) / Q chains
 // (ds_bpermute shifts, canonical mulm at every step).
 // ---------------------------------------------------------------------------
-// x * y mod q for |x|, |y| < 2^17: the 48-bit product as v_mul_i32_i24 +
-// v_mul_hi_i32_i24, reduced with 2^32 = 1 and 2^16 = -1: |result| < 65600
-__device__ __forceinline__ int32_t mul_lz(int32_t x, int32_t y)
-{
-    uint32_t lo;
-    int32_t hi;
-    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(lo) : "v"(x), "v"(y));
-    asm("v_mul_hi_i32_i24 %0, %1, %2" : "=v"(hi) : "v"(x), "v"(y));
-    return static_cast<int32_t>(lo & 0xffffu) - static_cast<int32_t>(lo >> 16) + hi;
-}
-
-// canonical residue of |y| < 98305 (fold -> [-2, 65537], then +-q)
-__device__ __forceinline__ uint32_t canon_lz(int32_t y)
-{
-    const int32_t f = fold(y);
-    const int32_t c = f < 0 ? f + 65537 : f;
-    return static_cast<uint32_t>(c >= 65537 ? c - 65537 : c);
-}
-
-// x^(2^16 - 1) = x^-1 (x != 0) by the chain x^(2^2-1), x^(2^4-1),
-// x^(2^8-1), x^(2^16-1): 15 squarings + 4 multiplies, all lazy
-__device__ __forceinline__ uint32_t inv_lz(uint32_t xc)
-{
-    const int32_t x = balanced(xc);
-    const int32_t e2 = mul_lz(mul_lz(x, x), x);        // x^3
-    int32_t t = mul_lz(e2, e2);
-    t = mul_lz(t, t);                                  // x^12
-    const int32_t e4 = mul_lz(t, e2);                  // x^15
-    t = e4;
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-        t = mul_lz(t, t);
-    const int32_t e8 = mul_lz(t, e4);                  // x^255
-    t = e8;
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-        t = mul_lz(t, t);
-    return canon_lz(mul_lz(t, e8));                    // x^65535
-}
-
 // entries a row may hold (coef_ok on a canonical residue): the dot2 kernel
 // needs |balanced| <= 32766, the i8 split anything but 32640
 __device__ __forceinline__ bool coef_bad(uint32_t e)
