@@ -1782,7 +1782,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     // row block j of this wave over its super tile (columns col0 ..
     // col0 + 63) from image img
     auto compute = [&](const uint8_t* img, long long col0, int n_lm, const int* mi,
-                       const uint32_t* mc, auto jc) {
+                       const uint32_t* mc, auto jc, auto&& before_stores) {
         constexpr int j = decltype(jc)::value;
         auto* lds = (__attribute__((address_space(3))) const uint8_t*)img;
         const int t = 16 * rbj[j] + tl;
@@ -1881,11 +1881,18 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        qi_v4u v2[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int orow = 8 * h + (l >> 3), c = l & 7;
-            const qi_v4u v =
-                *reinterpret_cast<const qi_v4u*>(stg + orow * O::kStagePitch + 16 * c);
+            v2[h] = *reinterpret_cast<const qi_v4u*>(stg + orow * O::kStagePitch + 16 * c);
+        }
+        if constexpr (j == RPW - 1)
+            before_stores();
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int orow = 8 * h + (l >> 3), c = l & 7;
+            const qi_v4u v = v2[h];
             const int ot = 16 * rbj[j] + orow;
             const uint32_t vo = (act[j] && ot < L.R)
                                     ? static_cast<uint32_t>(pr[j][1 + h]) * ors +
@@ -1895,6 +1902,14 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+    };
+
+    auto idle_stores = [&]() {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+            __builtin_amdgcn_raw_buffer_store_b128(qi_v4u{0u, 0u, 0u, 0u}, go.r,
+                                                   static_cast<int>(0x80000000u + 16 * h), 0,
+                                                   kAuxStMf);
     };
 
     if (t0 >= t1)
@@ -1913,16 +1928,34 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         if (more)
             issue_rows(tile + 1);
         const long long col0 = static_cast<long long>(tile) * NCOL + 64 * st;
+        // an idle wave (row block past RB) issues the same two stores, past
+        // the buffer's extent (dropped): with the store count equal on both
+        // sides of the branch, the compiler's vmcnt wait for the next tile's
+        // rows stays behind them instead of draining this tile's stores
+        // (vmcnt(0) on the merged path)
+        // the next tile's rows go to LDS before this tile's stores issue: on
+        // gfx9 loads and stores share vmcnt, so waiting for the rows after
+        // the stores drained the stores too (the whole store latency per
+        // tile); here the wait covers the rows (issued at the top of the
+        // iteration) and the previous tile's stores
+        // (KS >= 8: k128 encode 0.985 -> 0.917 ms, k200 0.70 -> 0.67 ms; the
+        // short KS = 4 decodes keep the rows after the stores: cfg3 decode
+        // 0.186 vs 0.192 ms, gpurun_out ab_ws)
+        constexpr bool rows_first = KS >= 8;
+        auto stage_next = [&]() {
+            if (rows_first && more)
+                write_rows(img(b ^ 1));
+        };
         [&]<int... J>(std::integer_sequence<int, J...>) {
             ((act[J] ? compute(img(b), col0, nl[b], s_i(b), s_col(b),
-                               std::integral_constant<int, J>{})
-                     : void()),
+                               std::integral_constant<int, J>{}, stage_next)
+                     : (J == RPW - 1 ? (stage_next(), idle_stores()) : idle_stores())),
              ...);
         }(std::make_integer_sequence<int, RPW>{});
-        if (more) {
+        if (!rows_first && more)
             write_rows(img(b ^ 1));
+        if (more)
             nl[b ^ 1] = stage_marks(tile + 1, b ^ 1);
-        }
         __syncthreads();
     }
 }
