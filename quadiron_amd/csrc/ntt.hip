@@ -241,60 +241,83 @@ struct NttCtxArgs {
     long long cs;
 };
 
+// a * b mod q for a, b in [0, 65536] on the full-rate 24-bit multipliers:
+// the 48-bit product is hi 2^32 + lo (hi <= 1), and with 2^32 = 1, 2^16 = -1
+// it reduces to hi + lo16 - lo_hi16 in [-65535, 65536]
+__device__ __forceinline__ uint32_t mulm24(uint32_t a, uint32_t b)
+{
+    uint32_t lo, hi;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(lo) : "v"(a), "v"(b));
+    asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(hi) : "v"(a), "v"(b));
+    const int32_t v = static_cast<int32_t>(hi + (lo & 0xffffu)) - static_cast<int32_t>(lo >> 16);
+    return static_cast<uint32_t>(v < 0 ? v + 65537 : v);
+}
+
+constexpr int kCtxChains = 4;  // independent product chains per thread
+
+// The per-pattern constants as independent products, one item per thread
+// (DecodeContext::init, src/fec_context.h:232-274, restated):
+//   item j < len_2k:   C[j] = -A(w2k^j) / len_2k,  A(z) = prod_i (z - x_i)
+//   item len_2k + i:   1 / (x_i A'(x_i)),          A'(x_i) = prod_{j != i} (x_i - x_j)
+// so no coefficient of A is ever formed: the reference builds A by k
+// in-place multiplications by (x - x_i) and evaluates FFT_2k(A); one
+// workgroup per stripe doing that here was a chain of k barriers plus
+// O(len_2k k / 256) serial Horner steps per thread (k = 1000: 1.13 ms per
+// 16 stripes).  Grid (stripes, item blocks); every block stages the stripe's
+// x_i = r^id_i in LDS and each thread multiplies kCtxChains interleaved
+// partial products (j = c mod kCtxChains) so the multiplies pipeline.
+// Block (s, 0) also writes ids[] and posmap[].
 __global__ __launch_bounds__(kNttBlock) void ntt_ctx_kernel(NttCtxArgs a)
 {
-    extern __shared__ uint32_t A[];  // k + 1 coefficients of A(x)
+    extern __shared__ uint32_t xs[];  // x_i, padded to kCtxChains with "x = z"
     const int s = blockIdx.x, tid = threadIdx.x, k = a.L.k;
+    const int kp = (k + kCtxChains - 1) / kCtxChains * kCtxChains;
     int32_t* ctx = a.ctx + s * a.cs;
     int32_t* invA = ctx;
     int32_t* C = ctx + a.L.c_off();
     int32_t* posmap = ctx + a.L.pos_off();
     int32_t* ids = ctx + a.L.ids_off();
-    for (int i = tid; i < k; i += kNttBlock) {
-        const int id = a.ids ? a.ids[static_cast<long long>(s) * k + i] : i;
-        ids[i] = id;
-        invA[i] = static_cast<int32_t>(powm_(a.r, static_cast<uint32_t>(id)));  // x_i for now
+    const uint16_t* sid = a.ids ? a.ids + static_cast<long long>(s) * k : nullptr;
+    for (int i = tid; i < kp; i += kNttBlock)
+        xs[i] = i < k ? powm_(a.r, sid ? sid[i] : static_cast<uint32_t>(i)) : 0xffffffffu;
+    if (blockIdx.y == 0) {
+        for (int t = tid; t < a.L.n; t += kNttBlock)
+            posmap[t] = -1;
     }
-    for (int d = tid; d <= k; d += kNttBlock)
-        A[d] = d == 0 ? 1u : 0u;
-    for (int t = tid; t < a.L.n; t += kNttBlock)
-        posmap[t] = -1;
     __syncthreads();
-    // A(x) = prod_i (x - x_i)  (Poly::mul_to_x_plus_coef, src/vec_poly.h):
-    // A <- A (x - x_i) in place, each thread on a contiguous chunk of
-    // coefficients from the top down, the chunk's lower neighbour value
-    // saved before the update
-    const int chunk = (k + 1 + kNttBlock - 1) / kNttBlock;
-    const int lo = tid * chunk, hi = min(lo + chunk, k + 1);
-    for (int i = 0; i < k; i++) {
-        const uint32_t xi = static_cast<uint32_t>(invA[i]);
-        const int top = min(hi - 1, i + 1);
-        const uint32_t below = (lo >= 1 && lo <= top) ? A[lo - 1] : 0u;
-        __syncthreads();
-        for (int d = top; d >= lo; d--) {
-            const uint32_t lowr = d == 0 ? 0u : (d - 1 >= lo ? A[d - 1] : below);
-            A[d] = subm_(lowr, mulm_(xi, A[d]));
+    if (blockIdx.y == 0) {
+        for (int i = tid; i < k; i += kNttBlock) {
+            const int id = sid ? sid[i] : i;
+            ids[i] = id;
+            posmap[id] = i;
         }
-        __syncthreads();
     }
-    // 1 / (x_i A'(x_i)): A' by Horner on d A[d]
-    for (int i = tid; i < k; i += kNttBlock) {
-        const uint32_t xi = static_cast<uint32_t>(invA[i]);
-        uint32_t acc = 0;
-        for (int d = k; d >= 1; d--)
-            acc = addm_(mulm_(acc, xi), mulm_(A[d], static_cast<uint32_t>(d)));
-        invA[i] = static_cast<int32_t>(powm_(mulm_(acc, xi), 65535u));
-        posmap[ids[i]] = i;
+    const int u = blockIdx.y * kNttBlock + tid;
+    const int len2k = a.L.len2k;
+    if (u >= len2k + k)
+        return;
+    const bool is_c = u < len2k;
+    const int self = is_c ? -1 : u - len2k;
+    const uint32_t z = is_c ? powm_(a.w2k, static_cast<uint32_t>(u)) : xs[self];
+    uint32_t acc[kCtxChains];
+#pragma unroll
+    for (int c = 0; c < kCtxChains; c++)
+        acc[c] = 1;
+    // padding entries (0xffffffff) and x_self contribute a factor 1
+    for (int j = 0; j < kp; j += kCtxChains) {
+        const uint4 xv = *reinterpret_cast<const uint4*>(xs + j);
+        const uint32_t xj[kCtxChains] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int c = 0; c < kCtxChains; c++) {
+            const bool one = xj[c] == 0xffffffffu || j + c == self;
+            acc[c] = mulm24(acc[c], one ? 1u : subm_(z, xj[c]));
+        }
     }
-    // C[j] = -A(w2k^j) / len_2k  (FFT_2k(A) with ifft's scale and the final
-    // negation of decode_apply folded in)
-    for (int j = tid; j < a.L.len2k; j += kNttBlock) {
-        const uint32_t xj = powm_(a.w2k, static_cast<uint32_t>(j));
-        uint32_t acc = 0;
-        for (int d = k; d >= 0; d--)
-            acc = addm_(mulm_(acc, xj), A[d]);
-        C[j] = static_cast<int32_t>(subm_(0u, mulm_(acc, a.inv_len2k)));
-    }
+    uint32_t p = mulm24(mulm24(acc[0], acc[1]), mulm24(acc[2], acc[3]));
+    if (is_c)
+        C[u] = static_cast<int32_t>(subm_(0u, mulm24(p, a.inv_len2k)));
+    else
+        invA[self] = static_cast<int32_t>(powm_(mulm24(p, z), 65535u));
 }
 
 // decode step 1: received row i of stripe s -> scratch row i, y = v inv_A_i
@@ -431,6 +454,8 @@ struct NttLdsArgs {
     int out_first, out_rows;  // sequence index of output row 0, row count
     Oor out_oor;
     uint32_t* err;
+    int wide;  // 16-byte row pieces: every row base and stride 8-word
+               // aligned and words % 8 == 0 (lds_launch checks)
 };
 
 // One pass over the image: tasks (group start b, offset j < s) of the R
@@ -515,8 +540,16 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     int32_t* s_inv = tw + a.tw_words;          // inv_A_i (balanced)
     int32_t* s_id = s_inv + k;                 // received ids z_i
     int32_t* s_c = s_id + k;                   // C[j] (balanced), natural order
-    const int s = blockIdx.x / a.tiles;
-    const long long c0 = static_cast<long long>(blockIdx.x - s * a.tiles) << lgT;
+    // XCD-aware map: workgroups go round-robin over the 8 XCDs (b % 8), and
+    // a tile is only T = 8..64 columns (16..128 bytes of a row), so in
+    // stripe-major order the tiles sharing a 128-byte line ran on different
+    // XCDs (each L2 fetching and partially writing the same lines).  XCD x
+    // walks the contiguous eighth x of the (stripe, tile) order instead.
+    int b = blockIdx.x;
+    if ((gridDim.x & 7) == 0)
+        b = (b & 7) * static_cast<int>(gridDim.x >> 3) + (b >> 3);
+    const int s = b / a.tiles;
+    const long long c0 = static_cast<long long>(b - s * a.tiles) << lgT;
     const int tid = threadIdx.x, col = tid & (T - 1), g = tid >> lgT, G = kLdsThreads >> lgT;
     const long long cg = c0 + col;
     const bool valid = cg < a.words;
@@ -539,7 +572,58 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
         return id < src.split ? src.base0 + s * src.ss0 + id * src.rs0
                               : src.base1 + s * src.ss1 + (id - src.split) * src.rs1;
     };
-    if (!dec) {
+    // wide row pieces: lane (rl, cj) moves columns 8 cj .. 8 cj + 7 of a
+    // row as one 16-byte access (a wave covers 64 / LPR rows); otherwise a
+    // lane moves one u16 column and a wave 64 / T rows of T columns, i.e.
+    // 16..128-byte pieces per wave instruction and few bytes in flight
+    const int lgL = lgT - 3, rl = tid >> lgL, cj = tid & ((1 << lgL) - 1);
+    const int RPP = kLdsThreads >> lgL;  // rows per sweep
+    const long long cw = c0 + 8 * cj;    // first column of the lane's piece
+    const bool wvalid = cw < a.words;
+    auto ld_piece = [&](int id) {
+        const uint16_t* r = row_ptr(id) + cw;
+        return *reinterpret_cast<const uint4*>(r);
+    };
+    // 8 u16 (a uint4) -> int32 words at image row p, columns 8 cj ..
+    auto put_piece = [&](int p, uint4 x, int32_t scale, bool sc) {
+        int4 lo, hi;
+        const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+        int32_t e[8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            e[2 * q] = static_cast<int32_t>(xs[q] & 0xffffu);
+            e[2 * q + 1] = static_cast<int32_t>(xs[q] >> 16);
+        }
+        if (sc) {
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                e[q] = mul_rt(e[q], scale);
+        }
+        lo = int4{e[0], e[1], e[2], e[3]};
+        hi = int4{e[4], e[5], e[6], e[7]};
+        int4* d = reinterpret_cast<int4*>(buf + (p << lgT) + 8 * cj);
+        d[0] = lo;
+        d[1] = hi;
+    };
+    if (!dec && a.wide) {
+        // data rows t < k at natural positions, zero above (DIF input)
+        for (int p0 = rl; p0 < a.n; p0 += RPP * kLdsBatch) {
+            uint4 x[kLdsBatch];
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) {
+                const int p = p0 + u * RPP;
+                x[u] = (p < k && wvalid) ? ld_piece(p) : uint4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < kLdsBatch; u++) {
+                const int p = p0 + u * RPP;
+                if (p < a.n)
+                    put_piece(p, x[u], 0, false);
+            }
+        }
+        __syncthreads();
+        lds_transform<true, false>(buf, tw, a.pnf, lgT, col, g, G);
+    } else if (!dec) {
         // data rows t < k at natural positions, zero above (DIF input);
         // kLdsBatch row loads in flight per thread
         for (int p0 = g; p0 < a.n; p0 += G * kLdsBatch) {
@@ -563,6 +647,23 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
         for (int p = g; p < a.n; p += G)
             buf[(p << lgT) + col] = 0;
         __syncthreads();
+        if (a.wide) {
+            for (int i0 = rl; i0 < k; i0 += RPP * kLdsBatch) {
+                uint4 x[kLdsBatch];
+#pragma unroll
+                for (int u = 0; u < kLdsBatch; u++) {
+                    const int i = i0 + u * RPP;
+                    x[u] = (i < k && wvalid) ? ld_piece(src.by_pos ? i : s_id[i])
+                                             : uint4{0, 0, 0, 0};
+                }
+#pragma unroll
+                for (int u = 0; u < kLdsBatch; u++) {
+                    const int i = i0 + u * RPP;
+                    if (i < k)
+                        put_piece(xf_pos(a.pnf, s_id[i]), x[u], s_inv[i], true);
+                }
+            }
+        } else
         for (int i0 = g; i0 < k; i0 += G * kLdsBatch) {
             int32_t x[kLdsBatch];
 #pragma unroll
@@ -626,9 +727,46 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     }
     // output rows: sequence index t = out_first + r, at position t (DIT
     // output: natural order) or pos_n(t) (DIF output)
+    const bool natural = a.mode == kLdsDec;
+    if (a.wide) {
+        if (!wvalid)
+            return;
+        for (int r = rl; r < a.out_rows; r += RPP) {
+            const int t = a.out_first + r;
+            const int p = natural ? t : xf_pos(a.pnf, t);
+            const int4* sp = reinterpret_cast<const int4*>(buf + (p << lgT) + 8 * cj);
+            const int4 lo = sp[0], hi = sp[1];
+            const int32_t e[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            uint32_t cv[8];
+            bool any = false;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                cv[q] = canon_vr(e[q]);
+                any |= cv[q] == 65536u;
+            }
+            uint4 o;
+            o.x = (cv[0] & 0xffffu) | (cv[1] << 16);
+            o.y = (cv[2] & 0xffffu) | (cv[3] << 16);
+            o.z = (cv[4] & 0xffffu) | (cv[5] << 16);
+            o.w = (cv[6] & 0xffffu) | (cv[7] << 16);
+            *reinterpret_cast<uint4*>(a.out + s * a.oss + r * a.ors + cw) = o;
+            if (any && a.out_oor.counts) {
+                const long long bk = static_cast<long long>(s) * a.out_oor.slots + r;
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    if (cv[q] == 65536u) {
+                        const uint32_t en = atomicAdd(&a.out_oor.counts[bk], 1u);
+                        if (en < static_cast<uint32_t>(a.out_oor.cap))
+                            a.out_oor.entries[bk * a.out_oor.cap + en] =
+                                static_cast<uint32_t>(cw + q);
+                    }
+                }
+            }
+        }
+        return;
+    }
     if (!valid)
         return;
-    const bool natural = a.mode == kLdsDec;
     for (int r = g; r < a.out_rows; r += G) {
         const int t = a.out_first + r;
         const int p = natural ? t : xf_pos(a.pnf, t);
@@ -877,6 +1015,14 @@ int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
     if (tiles * S > 0x7fffffffLL)
         return -3;
     a.tiles = static_cast<int>(tiles);
+    {
+        auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+        auto a8 = [](long long v) { return (v & 7) == 0; };
+        const RowSrc& r = a.src;
+        a.wide = (a.words & 7) == 0 && al(r.base0) && a8(r.ss0) && a8(r.rs0) &&
+                 (!r.base1 || (al(r.base1) && a8(r.ss1) && a8(r.rs1))) && al(a.out) &&
+                 a8(a.oss) && a8(a.ors);
+    }
     const size_t lds = lds_bytes(p, a.lgT, a.tw_words);
     if (lds > 65536 &&
         hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_lds_kernel),
@@ -969,12 +1115,15 @@ int ntt_build_ctx(const qi_plan* p, const uint16_t* d_ids, int S, int32_t* ctx, 
         return 0;
     NttCtxArgs a{ctx_layout_of(p), p->r, root_of_unity(static_cast<uint32_t>(p->len2k)),
                  invmod_c(static_cast<uint32_t>(p->len2k)), d_ids, ctx, cs};
-    const size_t lds = static_cast<size_t>(p->k + 1) * 4;
+    const size_t lds =
+        static_cast<size_t>((p->k + kCtxChains - 1) / kCtxChains * kCtxChains) * 4;
     if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_ctx_kernel),
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            static_cast<int>(lds)) != hipSuccess)
         return -2;
-    hipLaunchKernelGGL(ntt_ctx_kernel, dim3(S), dim3(kNttBlock), lds, st, a);
+    const int items = p->len2k + p->k;
+    hipLaunchKernelGGL(ntt_ctx_kernel, dim3(S, (items + kNttBlock - 1) / kNttBlock),
+                       dim3(kNttBlock), lds, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
