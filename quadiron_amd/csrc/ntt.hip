@@ -422,6 +422,10 @@ __device__ __forceinline__ int xf_pos(const XfPlan& P, int t)
     }
     return p;
 }
+__device__ __forceinline__ int ilog2_dev(int n)
+{
+    return 31 - __builtin_clz(static_cast<unsigned>(n));
+}
 __device__ __forceinline__ int xf_index(const XfPlan& P, int p)
 {
     int t = 0, b = 0;
@@ -440,7 +444,8 @@ struct NttLdsArgs {
     int lgT, tiles;
     long long words;
     // NTT_n / INTT_n / NTT_2k / INTT_2k: geometry + pass table offsets
-    XfPlan pnf, pni, p2f, p2i;
+    XfPlan pnf, pni, p2f, p2i;  // p2f / p2i: NTT_h / INTT_h, h = len_2k / 2
+    int twist;          // w2k^t, then w2k^-t (t < h), in the table range
     const int32_t* tw;  // the pass twiddle tables (qi_plan::d_ldstw)
     int tw_words;
     RowSrc src;         // enc: data rows by position; dec: received rows
@@ -463,60 +468,101 @@ struct NttLdsArgs {
 // w_L^{j u}; DIT: input q times w_L^{+-j q}, then codelet.  A task's
 // twiddles are contiguous in the pass table (vector LDS reads) and its R
 // elements sit at one base plus loop-invariant strides.
-template <int R, bool DIF, bool INV>
-__device__ __forceinline__ void lds_pass(int32_t* buf, const int32_t* twp, int N, int lgs,
-                                         int lgL, int lgT, int col, int g, int G)
+// UNIT: the s = 1 pass, whose twiddles w_L^{0 u} are all 1 (no table reads,
+// no multiplies).  Optional output scale (the decode's x C, fused into the
+// last DIF pass of NTT_2k): element u of task tt sits at position tt R + u,
+// i.e. holds X[xf_index(tt R) + (u << cb)], times cm[that] (canonical when
+// CANON, else balanced).
+template <int R, bool DIF, bool INV, bool UNIT, bool CANON>
+__device__ __forceinline__ void lds_pass_body(int32_t* buf, const int32_t* twp, int N, int lgs,
+                                              int lgL, int lgT, int col, int g, int G,
+                                              const int32_t* cm, int cb, const XfPlan* cp,
+                                              int lgnb)
 {
-    const int tasks = N / R, sE = (1 << lgs) << lgT;
-    for (int tt = g; tt < tasks; tt += G) {
-        const int j = tt & ((1 << lgs) - 1);
-        int32_t* e = buf + ((((tt >> lgs) << lgL) + j) << lgT) + col;
+    const int lgtasks = ilog2_dev(N) - ilog2_dev(R);
+    for (int t2 = g; t2 < (1 << (lgtasks + lgnb)); t2 += G) {
+        // transform bi of the batch (at image row bi N), its task tt
+        const int bi = t2 >> lgtasks, tt = t2 & ((1 << lgtasks) - 1);
+        const int j = UNIT ? 0 : tt & ((1 << lgs) - 1);
+        const int lb = ((bi * N + ((tt >> lgs) << lgL) + j) << lgT) + col;
         const int32_t* tj = twp + j * R;
         int32_t v[R], w[R];
 #pragma unroll
         for (int q = 0; q < R; q++) {
-            v[q] = e[q * sE];
-            w[q] = tj[q];
+            v[q] = buf[lb + ((q << lgs) << lgT)];
+            if (!UNIT)
+                w[q] = tj[q];
         }
-        if (!DIF) {
+        if (!DIF && !UNIT) {
 #pragma unroll
             for (int q = 1; q < R; q++)
                 v[q] = mul_rt(v[q], w[q]);
         }
         dft<R, kInLo, kInHi>(v);
+        int ci0 = 0;
+        if (UNIT && DIF && cm)
+            ci0 = xf_index(*cp, tt * R);
 #pragma unroll
         for (int u = 0; u < R; u++) {
             int32_t y = v[INV ? (R - u) % R : u];
-            if (DIF && u > 0)
+            if (DIF && !UNIT && u > 0)
                 y = mul_rt(y, w[u]);
-            e[u * sE] = y;
+            if (UNIT && DIF && cm) {
+                const int32_t c = cm[((ci0 + (u << cb)) << lgnb) + bi];
+                y = mul_rt(y, CANON ? balanced(static_cast<uint32_t>(c)) : c);
+            }
+            buf[lb + ((u << lgs) << lgT)] = y;
         }
     }
 }
 
-template <bool DIF, bool INV>
-__device__ void lds_transform(int32_t* buf, const int32_t* tw, const XfPlan& P, int lgT,
-                              int col, int g, int G)
+template <int R, bool DIF, bool INV, bool CANON>
+__device__ __forceinline__ void lds_pass(int32_t* buf, const int32_t* twp, int N, int lgs,
+                                         int lgL, int lgT, int col, int g, int G,
+                                         const int32_t* cm, int cb, const XfPlan* cp, int lgnb)
 {
+    if (lgs == 0)
+        lds_pass_body<R, DIF, INV, true, CANON>(buf, twp, N, lgs, lgL, lgT, col, g, G, cm, cb,
+                                                cp, lgnb);
+    else
+        lds_pass_body<R, DIF, INV, false, CANON>(buf, twp, N, lgs, lgL, lgT, col, g, G,
+                                                 nullptr, 0, cp, lgnb);
+}
+
+// cm (DIF only): the output scale of the last (s = 1) pass, indexed by the
+// natural output index (see lds_pass_body).  2^lgnb transforms of P.N
+// points back to back (image rows bi N ..), the same passes over all: the
+// scale of output m of transform bi is cm[(m << lgnb) + bi].
+template <bool DIF, bool INV, bool CANON = false>
+__device__ void lds_transform(int32_t* buf, const int32_t* tw, const XfPlan& P, int lgT,
+                              int col, int g, int G, const int32_t* cm = nullptr, int lgnb = 0)
+{
+    const int cb = P.N == 1 ? 0 : ilog2_dev(P.N) - P.lgr[P.np - 1];
     for (int i = 0; i < P.np; i++) {
         const int q = DIF ? i : P.np - 1 - i;  // DIT: the passes in reverse
         const int lgs = P.sh[q], lgL = lgs + P.lgr[q];
         const int32_t* twp = tw + P.tw[q];
+        const int32_t* c = DIF && i == P.np - 1 ? cm : nullptr;
         switch (P.lgr[q]) {
         case 1:
-            lds_pass<2, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
+            lds_pass<2, DIF, INV, CANON>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, c, cb, &P,
+                                           lgnb);
             break;
         case 2:
-            lds_pass<4, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
+            lds_pass<4, DIF, INV, CANON>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, c, cb, &P,
+                                           lgnb);
             break;
         case 3:
-            lds_pass<8, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
+            lds_pass<8, DIF, INV, CANON>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, c, cb, &P,
+                                           lgnb);
             break;
         case 4:
-            lds_pass<16, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
+            lds_pass<16, DIF, INV, CANON>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, c, cb, &P,
+                                           lgnb);
             break;
         default:
-            lds_pass<32, DIF, INV>(buf, twp, P.N, lgs, lgL, lgT, col, g, G);
+            lds_pass<32, DIF, INV, CANON>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, c, cb, &P,
+                                           lgnb);
             break;
         }
         __syncthreads();
@@ -524,20 +570,26 @@ __device__ void lds_transform(int32_t* buf, const int32_t* tw, const XfPlan& P, 
 }
 
 // LDS side arrays behind the nmax x T image (int32 words)
-__host__ __device__ inline int lds_side_words(int tw_words, int k, int len2k)
+__host__ __device__ inline int lds_side_words(int tw_words, int k, int len2k, bool twg)
 {
-    return tw_words + 2 * k + len2k;
+    return twg ? 2 * k : tw_words + 2 * k + len2k;
 }
 
 constexpr int kLdsBatch = 8;  // row loads in flight per thread
 
+// TWG: the pass twiddle tables and C are read from global memory (L1/L2
+// hits) instead of being staged in LDS, so that two workgroups fit a CU
+// where the staged tables would leave room for one (lds_geom; k1000 decode:
+// 64 KB image + 8 KB of ids / inv_A instead of + 38 KB)
+template <bool TWG>
 __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
 {
     extern __shared__ int32_t qi_ntt_lds[];
     const int nmax = a.nmax, lgT = a.lgT, T = 1 << lgT, k = a.k;
     int32_t* buf = qi_ntt_lds;
-    int32_t* tw = qi_ntt_lds + (nmax << lgT);  // pass twiddle tables
-    int32_t* s_inv = tw + a.tw_words;          // inv_A_i (balanced)
+    int32_t* tw_l = qi_ntt_lds + (nmax << lgT);  // pass twiddle tables
+    const int32_t* tw = TWG ? a.tw : tw_l;
+    int32_t* s_inv = TWG ? tw_l : tw_l + a.tw_words;  // inv_A_i (balanced)
     int32_t* s_id = s_inv + k;                 // received ids z_i
     int32_t* s_c = s_id + k;                   // C[j] (balanced), natural order
     // XCD-aware map: workgroups go round-robin over the 8 XCDs (b % 8), and
@@ -557,15 +609,17 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     // every per-stripe constant into LDS first (one round of independent
     // loads), so the hot loops below wait on nothing but their row loads
     const int32_t* ctx = a.ctx + s * a.cs;
-    for (int e = tid; e < a.tw_words; e += kLdsThreads)
-        tw[e] = a.tw[e];
+    if (!TWG)
+        for (int e = tid; e < a.tw_words; e += kLdsThreads)
+            tw_l[e] = a.tw[e];
     if (dec) {
         for (int i = tid; i < k; i += kLdsThreads) {
             s_inv[i] = balanced(static_cast<uint32_t>(ctx[i]));
             s_id[i] = ctx[a.ids_off + i];
         }
-        for (int j = tid; j < a.len2k; j += kLdsThreads)
-            s_c[j] = balanced(static_cast<uint32_t>(ctx[a.c_off + j]));
+        if (!TWG)
+            for (int j = tid; j < a.len2k; j += kLdsThreads)
+                s_c[j] = balanced(static_cast<uint32_t>(ctx[a.c_off + j]));
     }
     const RowSrc& src = a.src;
     auto row_ptr = [&](int id) {
@@ -601,7 +655,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
         }
         lo = int4{e[0], e[1], e[2], e[3]};
         hi = int4{e[4], e[5], e[6], e[7]};
-        int4* d = reinterpret_cast<int4*>(buf + (p << lgT) + 8 * cj);
+        int4* d = reinterpret_cast<int4*>(buf + ((p) << lgT) + 8 * cj);
         d[0] = lo;
         d[1] = hi;
     };
@@ -637,7 +691,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
             for (int u = 0; u < kLdsBatch; u++) {
                 const int p = p0 + u * G;
                 if (p < a.n)
-                    buf[(p << lgT) + col] = x[u];
+                    buf[((p) << lgT) + col] = x[u];
             }
         }
         __syncthreads();
@@ -645,7 +699,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     } else {
         // INTT_n input (DIT order): zero, then y_i = v_i inv_A_i at pos_n(z_i)
         for (int p = g; p < a.n; p += G)
-            buf[(p << lgT) + col] = 0;
+            buf[((p) << lgT) + col] = 0;
         __syncthreads();
         if (a.wide) {
             for (int i0 = rl; i0 < k; i0 += RPP * kLdsBatch) {
@@ -677,7 +731,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
             for (int u = 0; u < kLdsBatch; u++) {
                 const int i = i0 + u * G;
                 if (i < k)
-                    buf[(xf_pos(a.pnf, s_id[i]) << lgT) + col] = mul_rt(x[u], s_inv[i]);
+                    buf[((xf_pos(a.pnf, s_id[i])) << lgT) + col] = mul_rt(x[u], s_inv[i]);
             }
         }
         __syncthreads();
@@ -701,26 +755,41 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
                     const long long c = static_cast<long long>(
                                             a.in_oor.entries[bk * a.in_oor.cap + e]) - c0;
                     if (c >= 0 && c < T)
-                        buf[(p << lgT) + static_cast<int>(c)] = y;
+                        buf[((p) << lgT) + static_cast<int>(c)] = y;
                 }
             }
             __syncthreads();
         }
         lds_transform<false, true>(buf, tw, a.pni, lgT, col, g, G);
-        // first k outputs, zero-extended to len_2k; NTT_2k (DIF)
-        for (int p = k + g; p < a.len2k; p += G)
-            buf[(p << lgT) + col] = 0;
+        // NTT_2k of the first k outputs (zero from k, k <= h = len_2k / 2),
+        // x C, INTT_2k, split in halves (no pass touches the zero half):
+        //   X[2m] = NTT_h(x)[m],  X[2m+1] = NTT_h(x_t w2k^t)[m]
+        //   y_t = INTT_h(Y_even)[t] + w2k^-t INTT_h(Y_odd)[t]   (t < k)
+        // rows [0, h) hold the even transform, rows [h, 2h) the odd one
+        const int h = a.len2k >> 1;
+        const int32_t* twist = tw + a.twist;
+        for (int t = g; t < h; t += G) {
+            const int32_t x = t < k ? buf[(t << lgT) + col] : 0;
+            buf[(t << lgT) + col] = x;
+            buf[((h + t) << lgT) + col] = t < k ? mul_rt(x, twist[t]) : 0;
+        }
         __syncthreads();
-        lds_transform<true, false>(buf, tw, a.p2f, lgT, col, g, G);
-        // x C[j] (X[j] sits at pos_2k(j))
-        for (int p = g; p < a.len2k; p += G)
-            buf[(p << lgT) + col] = mul_rt(buf[(p << lgT) + col], s_c[xf_index(a.p2f, p)]);
+        // both NTT_h (DIF) at once, times C[2m + bi] in the last pass
+        if (TWG)
+            lds_transform<true, false, true>(buf, tw, a.p2f, lgT, col, g, G, ctx + a.c_off, 1);
+        else
+            lds_transform<true, false, false>(buf, tw, a.p2f, lgT, col, g, G, s_c, 1);
+        lds_transform<false, true>(buf, tw, a.p2i, lgT, col, g, G, nullptr, 1);
+        for (int t = g; t < k; t += G) {
+            const int32_t e = buf[(t << lgT) + col];
+            const int32_t o = mul_rt(buf[((h + t) << lgT) + col], twist[h + t]);
+            buf[(t << lgT) + col] = fold(e + o);  // [-65538, 131072] -> V range
+        }
         __syncthreads();
-        lds_transform<false, true>(buf, tw, a.p2i, lgT, col, g, G);
         if (a.mode != kLdsDec) {
             // systematic: evaluate the coefficients at r^t (NTT_n, DIF)
             for (int p = k + g; p < a.n; p += G)
-                buf[(p << lgT) + col] = 0;
+                buf[((p) << lgT) + col] = 0;
             __syncthreads();
             lds_transform<true, false>(buf, tw, a.pnf, lgT, col, g, G);
         }
@@ -734,7 +803,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
         for (int r = rl; r < a.out_rows; r += RPP) {
             const int t = a.out_first + r;
             const int p = natural ? t : xf_pos(a.pnf, t);
-            const int4* sp = reinterpret_cast<const int4*>(buf + (p << lgT) + 8 * cj);
+            const int4* sp = reinterpret_cast<const int4*>(buf + ((p) << lgT) + 8 * cj);
             const int4 lo = sp[0], hi = sp[1];
             const int32_t e[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
             uint32_t cv[8];
@@ -770,7 +839,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     for (int r = g; r < a.out_rows; r += G) {
         const int t = a.out_first + r;
         const int p = natural ? t : xf_pos(a.pnf, t);
-        const uint32_t cv = canon_vr(buf[(p << lgT) + col]);
+        const uint32_t cv = canon_vr(buf[((p) << lgT) + col]);
         a.out[s * a.oss + r * a.ors + cg] = static_cast<uint16_t>(cv);
         if (cv == 65536u && a.out_oor.counts) {
             const long long bk = static_cast<long long>(s) * a.out_oor.slots + r;
@@ -915,13 +984,30 @@ XfPlan xf_plan(int N)
 // non-systematic encode the last one, systematic codes all four.
 enum : int { kTwPni = 0, kTwP2f = 1, kTwP2i = 2, kTwPnf = 3 };
 
-int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab)
+int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab, int* twist = nullptr)
 {
     const uint32_t w = root_of_unity(static_cast<uint32_t>(p->nmax));
-    const int Ns[4] = {p->n, p->len2k, p->len2k, p->n};
+    const int h = p->len2k / 2;
+    const int Ns[4] = {p->n, h, h, p->n};
     const bool invs[4] = {true, false, true, false};
     int off = 0;
     for (int t = 0; t < 4; t++) {
+        if (t == kTwPnf) {
+            if (twist)
+                *twist = off;
+            // the decode's twist w2k^{+-t}, t < h, between INTT_h and NTT_n
+            // (a decode stages [0, NTT_n's offset))
+            if (tab) {
+                tab->resize(off + 2 * h);
+                const uint32_t w2 = powmod_c(w, static_cast<uint32_t>(p->nmax / p->len2k));
+                const uint32_t w2i = invmod_c(w2);
+                for (int i = 0; i < h; i++) {
+                    (*tab)[off + i] = balanced(powmod_c(w2, static_cast<uint32_t>(i)));
+                    (*tab)[off + h + i] = balanced(powmod_c(w2i, static_cast<uint32_t>(i)));
+                }
+            }
+            off += (2 * h + 3) & ~3;
+        }
         pl[t] = xf_plan(Ns[t]);
         const bool inv = invs[t];
         for (int q = 0; q < pl[t].np; q++) {
@@ -944,9 +1030,10 @@ int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab)
     return off;
 }
 
-size_t lds_bytes(const qi_plan* p, int lgT, int tw_words)
+size_t lds_bytes(const qi_plan* p, int lgT, int tw_words, bool twg)
 {
-    return ((static_cast<size_t>(p->nmax) << lgT) + lds_side_words(tw_words, p->k, p->len2k)) *
+    return ((static_cast<size_t>(p->nmax) << lgT) +
+            lds_side_words(tw_words, p->k, p->len2k, twg)) *
            4;
 }
 
@@ -967,13 +1054,19 @@ void lds_table_range(const qi_plan* p, int mode, int* lo, int* hi)
 }
 
 // columns per workgroup: the widest tile (<= 64 columns) that leaves room
-// for two workgroups per CU, else for one (at least 8 columns)
-int lds_lgT(const qi_plan* p, int tw_words)
+// for two workgroups per CU with the tables staged, else with the tables
+// read from global memory (*twg), else one workgroup per CU (at least 8
+// columns)
+int lds_geom(const qi_plan* p, int tw_words, bool* twg)
 {
-    for (int lg = 6; lg >= 3; lg--)
-        if (lds_bytes(p, lg, tw_words) <= kLdsCap / 2)
-            return lg;
-    return lds_bytes(p, 3, tw_words) <= kLdsCap ? 3 : -1;
+    for (int g = 0; g < 2; g++)
+        for (int lg = 6; lg >= 3; lg--)
+            if (lds_bytes(p, lg, tw_words, g == 1) <= kLdsCap / 2) {
+                *twg = g == 1;
+                return lg;
+            }
+    *twg = false;
+    return lds_bytes(p, 3, tw_words, false) <= kLdsCap ? 3 : -1;
 }
 
 bool lds_engine(const qi_plan* p)
@@ -982,7 +1075,8 @@ bool lds_engine(const qi_plan* p)
         return false;
     int lo, hi;
     lds_table_range(p, kLdsSysDec, &lo, &hi);  // the largest set
-    return lds_lgT(p, hi - lo) >= 0;
+    bool twg;
+    return lds_geom(p, hi - lo, &twg) >= 0;
 }
 
 int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
@@ -992,19 +1086,22 @@ int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
     a.len2k = p->len2k;
     a.nmax = p->nmax;
     XfPlan pl[4];
-    lds_tables(p, pl, nullptr);
+    int twist = 0;
+    lds_tables(p, pl, nullptr, &twist);
     int lo, hi;
     lds_table_range(p, a.mode, &lo, &hi);
     for (XfPlan& x : pl)
         for (int q = 0; q < x.np; q++)
             x.tw[q] -= lo;  // offsets within the staged range
+    a.twist = twist - lo;  // (read by decodes only, which stage from 0)
     a.pni = pl[kTwPni];
     a.p2f = pl[kTwP2f];
     a.p2i = pl[kTwP2i];
     a.pnf = pl[kTwPnf];
     a.tw = p->d_ldstw + lo;
     a.tw_words = hi - lo;
-    a.lgT = lds_lgT(p, a.tw_words);
+    bool twg;
+    a.lgT = lds_geom(p, a.tw_words, &twg);
     if (a.lgT < 0)
         return -3;
     const NttCtxLayout L = ctx_layout_of(p);
@@ -1023,14 +1120,18 @@ int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
                  (!r.base1 || (al(r.base1) && a8(r.ss1) && a8(r.rs1))) && al(a.out) &&
                  a8(a.oss) && a8(a.ors);
     }
-    const size_t lds = lds_bytes(p, a.lgT, a.tw_words);
-    if (lds > 65536 &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_lds_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(lds)) != hipSuccess)
+    const size_t lds = lds_bytes(p, a.lgT, a.tw_words, twg);
+    const void* fn = twg ? reinterpret_cast<const void*>(&ntt_lds_kernel<true>)
+                         : reinterpret_cast<const void*>(&ntt_lds_kernel<false>);
+    if (lds > 65536 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           static_cast<int>(lds)) != hipSuccess)
         return -2;
-    hipLaunchKernelGGL(ntt_lds_kernel, dim3(static_cast<unsigned>(tiles * S)),
-                       dim3(kLdsThreads), lds, st, a);
+    if (twg)
+        hipLaunchKernelGGL(ntt_lds_kernel<true>, dim3(static_cast<unsigned>(tiles * S)),
+                           dim3(kLdsThreads), lds, st, a);
+    else
+        hipLaunchKernelGGL(ntt_lds_kernel<false>, dim3(static_cast<unsigned>(tiles * S)),
+                           dim3(kLdsThreads), lds, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -149,9 +149,13 @@ def _ctx(k, n, len2k, ids):
 
 
 @pytest.mark.parametrize("k,m", [(65, 63), (100, 28), (40, 200)])
-def test_decode_pipeline(k, m):
+@pytest.mark.parametrize("split", [False, True])
+def test_decode_pipeline(k, m, split):
     """The kernel's decode order recovers the data polynomial's
-    coefficients from any k codeword symbols."""
+    coefficients from any k codeword symbols.  split: NTT_2k / INTT_2k as
+    the kernel runs them, two h = len_2k / 2 point transforms each
+    (X[2m] = NTT_h(x)[m], X[2m+1] = NTT_h(x_t w^t)[m]; y_t = INTT_h(even)[t]
+    + w^-t INTT_h(odd)[t]), C[2m + b] applied to output m of half b."""
     rng = random.Random(k * m)
     n = 1 << (k + m - 1).bit_length()
     len2k = 1 << (2 * k - 1).bit_length()
@@ -166,10 +170,27 @@ def test_decode_pipeline(k, m):
     for i, z in enumerate(ids):
         buf[xf_pos(pn, z)] = cw[z] * inv[i] % Q
     lds_transform(buf, n, pn, tables(pn, nmax, True), False, True)
-    for p in range(k, len2k):
-        buf[p] = 0
-    lds_transform(buf, len2k, p2, tables(p2, nmax, False), True, False)
-    for p in range(len2k):
-        buf[p] = buf[p] * C[xf_index(p2, p)] % Q
-    lds_transform(buf, len2k, p2, tables(p2, nmax, True), False, True)
-    assert buf[:k] == coef
+    if not split:
+        for p in range(k, len2k):
+            buf[p] = 0
+        lds_transform(buf, len2k, p2, tables(p2, nmax, False), True, False)
+        for p in range(len2k):
+            buf[p] = buf[p] * C[xf_index(p2, p)] % Q
+        lds_transform(buf, len2k, p2, tables(p2, nmax, True), False, True)
+        assert buf[:k] == coef
+        return
+    h = len2k // 2
+    w2 = root(len2k)
+    even = [buf[t] if t < k else 0 for t in range(h)]
+    odd = [even[t] * pow(w2, t, Q) % Q for t in range(h)]
+    ph = xf_plan(h)
+    out = []
+    for b, half in enumerate((even, odd)):
+        lds_transform(half, h, ph, tables(ph, nmax, False), True, False)
+        for p in range(h):
+            half[p] = half[p] * C[2 * xf_index(ph, p) + b] % Q
+        lds_transform(half, h, ph, tables(ph, nmax, True), False, True)
+        out.append(half)
+    w2i = pow(w2, Q - 2, Q)
+    y = [(out[0][t] + pow(w2i, t, Q) * out[1][t]) % Q for t in range(k)]
+    assert y == coef
