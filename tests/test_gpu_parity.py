@@ -254,6 +254,13 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
     (257, 255, 0, 1, 300),    # smallest NTT-path code
     (300, 100, 1, 1, 300),    # systematic: interpolation + NTT_n encode
     (1000, 24, 0, 1, 260),    # len_2k = 2048 > n = 1024
+    # the LDS engine's 16-byte row pieces (P % 8 == 0) and table placements:
+    # decode with ids / inv_A in the image rows INTT_n leaves free (n < nmax),
+    # tables from global memory (sys decode; n = nmax), tables staged
+    (1000, 24, 0, 2, 1024),
+    (1000, 24, 1, 1, 512),
+    (600, 1400, 0, 1, 256),   # n = len_2k = 2048: no free image rows
+    (385, 127, 0, 2, 1032),   # smallest k past the matrix path
 ])
 def test_batch_vs_oracle(k, m, sys_, S, P):
     _batch_roundtrip(k, m, sys_, S, P, seed=k * 1000 + m + P, n_craft=16)
