@@ -41,8 +41,14 @@
 // inverse twiddle table.
 //
 // The per-pattern context (DecodeContext::init, src/fec_context.h:232-274:
-// A(x) = prod (x - x_i), 1/(x_i A'(x_i)), FFT_2k(A)) is built on the GPU, one
-// workgroup per stripe, inside the caller's stream (no host round trip).
+// A(x) = prod (x - x_i), 1/(x_i A'(x_i)), FFT_2k(A)) is built on the GPU as
+// independent products over the received points (ntt_ctx_kernel), inside
+// the caller's stream (no host round trip).
+//
+// For max(n, len_2k) <= 2048 the whole pipeline of a column tile runs in LDS
+// (ntt_lds_kernel); there NTT_2k / INTT_2k run as two len_2k / 2 point
+// transforms each (the input's zero half and the output's unused half are
+// never transformed).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -580,7 +586,10 @@ constexpr int kLdsBatch = 8;  // row loads in flight per thread
 // TWG: the pass twiddle tables and C are read from global memory (L1/L2
 // hits) instead of being staged in LDS, so that two workgroups fit a CU
 // where the staged tables would leave room for one (lds_geom; k1000 decode:
-// 64 KB image + 8 KB of ids / inv_A instead of + 38 KB)
+// 64 KB image + 8 KB of ids / inv_A instead of + 38 KB).  Staging the pass
+// tables again with ids / inv_A in the image rows INTT_n leaves free (two
+// workgroups per CU, twist and C from global) measured slower: k1000 decode
+// 5.21 -> 5.45 ms (gpurun_out ntt6)
 template <bool TWG>
 __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
 {
