@@ -44,10 +44,24 @@ int qi_gpu_device_count(void);
 
 /* Create an RS-FNT plan (word_size 2 only).  Returns NULL on bad
  * parameters (k < 1, m < 1, k+m > 65536) or when no device is present.
- * k <= 256 runs the register-codelet (non-systematic k <= 32) and
- * matrix-core kernels, k > 256 the NTT-structured general path
- * (column-batched NTT passes). */
+ * Kernels by k:
+ *   - k <= 256: the register codelets (non-systematic encode, k <= 32) and
+ *     the matrix cores (every decode; the systematic encode; the
+ *     non-systematic encode for 32 < k <= 256), dot2 kernels for column
+ *     tails;
+ *   - 256 < k <= 384: the matrix cores for batches whose width is a
+ *     multiple of 1024 columns and whose rows are 8-byte aligned inside
+ *     31-bit buffer ranges (the encode only while the generator stays small:
+ *     k * n_outputs <= 2^21, 2^18 systematic); the NTT engine otherwise;
+ *   - k > 384: the NTT engine (column-batched NTT passes in LDS or HBM). */
 qi_plan* qi_plan_create(int k, int m, int systematic);
+/* The same with flags: QI_PLAN_ENC_MATRIX / QI_PLAN_ENC_CODELETS force the
+ * matrix-core or the register-codelet non-systematic encode for k <= 64
+ * (both bit-exact; the default picks the faster: codelets up to k = 32).
+ * NULL on unknown or contradictory flags. */
+#define QI_PLAN_ENC_MATRIX 1
+#define QI_PLAN_ENC_CODELETS 2
+qi_plan* qi_plan_create_ex(int k, int m, int systematic, int flags);
 void qi_plan_destroy(qi_plan* plan);
 /* n (FFT length) and n_outputs (m if systematic, k+m otherwise) */
 int qi_plan_n(const qi_plan* plan);
@@ -67,7 +81,10 @@ int qi_gpu_encode(qi_plan* plan, const uint16_t* d_data,
                   void* stream);
 
 /* Bytes of device workspace for n_stripes decode contexts of `words`
- * columns each. */
+ * columns each -- enough for any width up to `words`.  A context is valid
+ * only for the `words` it was built with (its format and per-stripe stride
+ * follow the width: for 256 < k <= 384, matrix contexts at multiples of
+ * 1024 columns, the NTT engine's otherwise). */
 size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
                                long long words);
 
@@ -76,11 +93,14 @@ size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
  * decoder uses (FecCode::decode_blocks_vertical picks the first k present,
  * src/fec_base.h:1199-1236) -- and route the OOR marks of those fragments
  * (buckets as produced by qi_gpu_encode; NULL counts = none) into per-tile
- * tables.  Built on the device, asynchronously on `stream`, for every k
- * (k <= 256: the interpolation matrix, up to ~780 KB per stripe at k = 256;
- * k > 256: the NTT decode's per-pattern constants, src/fec_context.h:232-274,
- * whose decode reads the OOR buckets directly).  h_ids is unused (kept for
- * ABI stability; may be NULL). */
+ * tables.  Built on the device, asynchronously on `stream`, for every k:
+ * matrix contexts (the interpolation matrix, up to ~780 KB per stripe at
+ * k = 256) for k <= 256, and for 256 < k <= 384 at widths that are a
+ * multiple of 1024 columns (then followed by the NTT engine's context, used
+ * when the decode's rows are not addressable by the matrix cores); the NTT
+ * decode's per-pattern constants (src/fec_context.h:232-274, whose decode
+ * reads the OOR buckets directly) otherwise.  h_ids is unused (kept for ABI
+ * stability; may be NULL). */
 int qi_gpu_decode_ctx(qi_plan* plan, const uint16_t* d_ids,
                       const uint16_t* h_ids, int n_stripes,
                       const uint32_t* d_oor_counts,

@@ -42,6 +42,7 @@ def _declare(lib):
         # include/qi_gpu.h
         "qi_gpu_device_count": (I, []),
         "qi_plan_create": (V, [I, I, I]),
+        "qi_plan_create_ex": (V, [I, I, I, I]),
         "qi_plan_destroy": (None, [V]),
         "qi_plan_n": (I, [V]),
         "qi_plan_n_outputs": (I, [V]),
@@ -160,10 +161,17 @@ def ptr_array(arrs):
 class Plan:
     """Device plan (include/qi_gpu.h) for RS-FNT(k, m)."""
 
-    def __init__(self, k, m, systematic=False):
+    ENCODERS = {None: 0, "matrix": 1, "codelets": 2}  # QI_PLAN_ENC_* flags
+
+    def __init__(self, k, m, systematic=False, encoder=None):
+        """encoder: None (the library's choice), "matrix" or "codelets"
+        (force the non-systematic encode kernel for k <= 64)."""
         require_device()
+        if encoder not in self.ENCODERS:
+            raise ValueError(f"encoder must be one of {list(self.ENCODERS)}")
         self.k, self.m, self.sys = k, m, bool(systematic)
-        self.h = lib().qi_plan_create(k, m, int(systematic))
+        self.h = lib().qi_plan_create_ex(k, m, int(systematic),
+                                         self.ENCODERS[encoder])
         if not self.h:
             raise ValueError(f"qi_plan_create({k}, {m}, {systematic}) failed")
         self.n = lib().qi_plan_n(self.h)

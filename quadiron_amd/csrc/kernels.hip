@@ -2263,22 +2263,37 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
 }
 
 
+// rows at `cols`-word aligned offsets (source regions and destination)
+static bool rows_aligned(int cols, const RowSrc& src, const RowDst& dst)
+{
+    return aligned_for(cols, src.base0, src.ss0, src.rs0, dst.ss, dst.rs) &&
+           (src.base1 == nullptr || aligned_for(cols, src.base1, src.ss1, src.rs1, 0, 0)) &&
+           (reinterpret_cast<uintptr_t>(dst.base) % (2 * cols)) == 0;
+}
+
+static MatExt mat_ext(const RowSrc& src, int R, const RowDst& dst, long long words)
+{
+    return MatExt{extent(src.rows0, src.rs0, words), extent(src.rows1, src.rs1, words),
+                  extent(R, dst.rs, words), 0};
+}
+
+bool matrix_cores_take(const RowSrc& src, const RowDst& dst, int R, long long words)
+{
+    const MatExt e = mat_ext(src, R, dst, words);
+    const bool buf = e.e0 && e.eo && (!src.base1 || e.e1);
+    return buf && rows_aligned(2, src, dst) && rows_aligned(4, src, dst) &&
+           words >= kRouteTile;
+}
+
 static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
 {
     const MatLayout& L = a.L;
     const RowSrc& src = a.src;
     const RowDst& dst = a.dst;
     const long long words = a.words;
-    const bool a2 = aligned_for(2, src.base0, src.ss0, src.rs0, dst.ss, dst.rs) &&
-                    (src.base1 == nullptr ||
-                     aligned_for(2, src.base1, src.ss1, src.rs1, 0, 0)) &&
-                    (reinterpret_cast<uintptr_t>(dst.base) % 4) == 0;
+    const bool a2 = rows_aligned(2, src, dst);
     const bool buf = a.ext.e0 && a.ext.eo && (!src.base1 || a.ext.e1);
-    const bool a4 = a2 &&
-                    aligned_for(4, src.base0, src.ss0, src.rs0, dst.ss, dst.rs) &&
-                    (src.base1 == nullptr ||
-                     aligned_for(4, src.base1, src.ss1, src.rs1, 0, 0)) &&
-                    (reinterpret_cast<uintptr_t>(dst.base) % 8) == 0;
+    const bool a4 = a2 && rows_aligned(4, src, dst);
     const int cols = !buf ? 1 : a4 ? 4 : a2 ? 2 : 1;
     // whole kRouteTile column tiles on the matrix cores, the tail (and
     // everything the MFMA kernel does not take) on the dot2 kernel
@@ -2323,13 +2338,15 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
     }
 }
 
-std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor)
+std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor, bool two)
 {
     // mirrors launch_matrix_kernels / mfma_dispatch / mat_dispatch for rows
-    // at 8-byte aligned offsets inside 31-bit buffer ranges
+    // at 8-byte aligned offsets inside 31-bit buffer ranges; the names are
+    // spelled as the demangler (and rocprofv3) spells the instantiations
     std::string r;
     const long long wfull = words / kRouteTile * kRouteTile;
     const int KS = L.KS();
+    auto tf = [](bool b) { return std::string(b ? "true" : "false"); };
     if (KS > 0 && wfull > 0) {
         const int RB = L.RB();
         int nst = KS == 1 ? 16 : 8, nw = 4;
@@ -2343,20 +2360,27 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
         }
         const OsGeom og = os_geom(KS, RB);
         if (og.wr)
-            r = "matrix_os_kernel<" + std::to_string(KS) + "," + std::to_string(og.wr) + "," +
-                std::to_string(og.rpw) + ">";
+            r = "matrix_os_kernel<" + std::to_string(KS) + ", " + std::to_string(og.wr) + ", " +
+                std::to_string(og.rpw) + ", " + tf(two) + ">";
         else
-            r = "matrix_mfma_kernel<" + std::to_string(KS) + "," + std::to_string(nst) + "," +
-                std::to_string(nw) + "," + (rsplit ? "true" : "false") + ">";
+            r = "matrix_mfma_kernel<" + std::to_string(KS) + ", " + std::to_string(nst) + ", " +
+                std::to_string(nw) + ", " + tf(rsplit) + ">";
     }
     if (wfull < words) {
         const int cols = L.KP <= 8 ? 4 : L.KP <= 16 ? 2 : 1;
         r += std::string(r.empty() ? "" : " + ") + "matrix_kernel<" + std::to_string(L.KP) +
-             "," + std::to_string(cols) + ",true> (tail)";
+             ", " + std::to_string(cols) + ", true> (tail)";
     }
     if (in_oor)
         r += " + matrix_redo_kernel";
     return r;
+}
+
+std::string encode_fnt_kernel_name(int k)
+{
+    const int K = static_cast<int>(ceil2(static_cast<uint32_t>(k)));
+    return "encode_fnt_kernel<" + std::to_string(K) + ", " + std::to_string(K <= 16 ? 2 : 1) +
+           ", " + (k == K ? "true" : "false") + ", true>";
 }
 
 int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
@@ -2372,10 +2396,7 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
     if (in_oor && !slow.base)
         return -1;  // input marks need the slow-tile lists
     const Oor none{nullptr, nullptr, 0, 0};
-    MatArgs a{L, mat, ms, ids, is, src, dst,
-              MatExt{extent(src.rows0, src.rs0, words), extent(src.rows1, src.rs1, words),
-                     extent(L.R, dst.rs, words), 0},
-              words, 0, in_oor ? *in_oor : none, slot_base, out_oor ? *out_oor : none,
+    MatArgs a{L, mat, ms, ids, is, src, dst, mat_ext(src, L.R, dst, words), words, 0, in_oor ? *in_oor : none, slot_base, out_oor ? *out_oor : none,
               rowmap, route, rstride, in_oor ? slow : SlowList{nullptr, 0}, err};
     const int rc = launch_matrix_kernels(a, S, st);
     if (rc || !in_oor)

@@ -1281,10 +1281,16 @@ int ntt_plan_init(qi_plan* p)
     return 0;
 }
 
-const char* ntt_engine_name(const qi_plan* p)
+std::string ntt_kernel_names(const qi_plan* p, bool decode)
 {
-    return lds_engine(p) ? "ntt_lds_kernel"
-                         : "ntt_pass_kernel (+ ntt_expand_kernel / ntt_fix_kernel)";
+    if (!lds_engine(p))
+        return decode ? "ntt_expand_kernel + ntt_fix_kernel + ntt_pass_kernel" : "ntt_pass_kernel";
+    const int mode = decode ? (p->sys ? kLdsSysDec : kLdsDec) : (p->sys ? kLdsSysEnc : kLdsEnc);
+    int lo, hi;
+    lds_table_range(p, mode, &lo, &hi);
+    bool twg;
+    (void)lds_geom(p, hi - lo, &twg);
+    return twg ? "ntt_lds_kernel<true>" : "ntt_lds_kernel<false>";
 }
 
 void ntt_plan_free(qi_plan* p)

@@ -2,7 +2,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -20,16 +19,27 @@ namespace qi {
 // (cfg3: 1.04 vs 1.17 ms, profiles/r2_ab_enc_matrix.txt): a 64-point
 // codelet pass needs ~15.5 VALU per output, the MFMA epilogue ~6.  At
 // K = 16 (cfg2) the codelets win (3.65 vs 3.75 ms).  K = 128, 256 have no
-// codelet (registers).  QI_ENC_MATRIX=1 / 0 forces either kernel at K <= 64 (A/B
-// and tests).
-static bool enc_matrix(int K)
+// codelet (registers).  QI_PLAN_ENC_MATRIX / QI_PLAN_ENC_CODELETS
+// (qi_plan_create_ex) force either kernel at K <= 64 (parity tests of both).
+static bool enc_matrix(int K, int flags)
 {
     if (K > 64)
         return true;
-    const char* e = std::getenv("QI_ENC_MATRIX");
-    if (e && (e[0] == '0' || e[0] == '1'))
-        return e[0] == '1';
+    if (flags & QI_PLAN_ENC_MATRIX)
+        return true;
+    if (flags & QI_PLAN_ENC_CODELETS)
+        return false;
     return K >= 64;
+}
+
+// 256 < k <= 384: the matrix-core encode's generator (n_outputs x k,
+// packed) is built only while it stays small; larger codes encode on the NTT
+// engine (a k = 384 generator for m near 65536 would take ~250 MB of device
+// memory and seconds of host time for the systematic Lagrange rows)
+static bool big_generator_ok(int k, int n_outputs, int sys)
+{
+    const long long e = static_cast<long long>(k) * n_outputs;
+    return e <= (sys ? (1LL << 18) : (1LL << 21));
 }
 
 static uint32_t addm(uint32_t a, uint32_t b)
@@ -145,6 +155,14 @@ int qi_gpu_device_count(void)
 
 qi_plan* qi_plan_create(int k, int m, int systematic)
 {
+    return qi_plan_create_ex(k, m, systematic, 0);
+}
+
+qi_plan* qi_plan_create_ex(int k, int m, int systematic, int flags)
+{
+    if (flags & ~(QI_PLAN_ENC_MATRIX | QI_PLAN_ENC_CODELETS) ||
+        (flags & QI_PLAN_ENC_MATRIX && flags & QI_PLAN_ENC_CODELETS))
+        return nullptr;
     if (k < 1 || m < 1 || k + m > 65536 || 2 * k >= 65537)
         return nullptr;
     if (qi_gpu_device_count() < 1)
@@ -175,7 +193,7 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
     if (ok && (!p->ntt || p->mbig)) {
         // twist factors w^{v t} for the encode passes (K <= 32; K = 64 to
         // 256 encode on the matrix cores)
-        if (!p->ntt && !p->sys && !enc_matrix(p->K)) {
+        if (!p->ntt && !p->sys && !enc_matrix(p->K, flags)) {
             const int passes = p->n / p->K;
             std::vector<int32_t> tw(static_cast<size_t>(passes) * p->K);
             for (int v = 0; v < passes; v++)
@@ -188,7 +206,9 @@ qi_plan* qi_plan_create(int k, int m, int systematic)
         }
         // generator matrix for the systematic encode (and the matrix-core
         // A/B knob of the non-systematic one): outputs x inputs
-        if (ok && (p->sys || p->mbig || enc_matrix(p->K))) {
+        const bool gen = p->mbig ? big_generator_ok(k, p->n_outputs, p->sys)
+                                 : p->sys || enc_matrix(p->K, flags);
+        if (ok && gen) {
             const int kp = matrix_kp(k);
             MatLayout L{p->n_outputs, k, kp};
             std::vector<uint32_t> M;

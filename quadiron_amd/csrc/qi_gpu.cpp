@@ -2,6 +2,7 @@
 // device-resident stripes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -25,13 +26,23 @@ hipStream_t st(void* s)
     return static_cast<hipStream_t>(s);
 }
 
-// the matrix path (contexts, kernels) for this batch width: every k <= 256,
-// and 256 < k <= 384 when the columns tile into whole 1024-column blocks
-// (the operand-stationary kernel has no column tail there); otherwise the
-// NTT engine
+// The decode-context format for this batch width: matrix contexts for
+// every k <= 256, and for 256 < k <= 384 (mbig) when the columns tile into
+// whole 1024-column blocks (the operand-stationary kernel has no column tail
+// there); otherwise the NTT engine's.  A context is valid only for the
+// `words` it was built with.
 bool use_matrix(const qi_plan* p, long long words)
 {
     return !p->ntt || (p->mbig && words % kRouteTile == 0);
+}
+
+// the matrix-format part of a context: packed block, ids, route table,
+// slow-tile list
+long long mat_ctx_words(const qi_plan* p, long long words)
+{
+    const MatLayout L = ctx_layout(p);
+    return static_cast<long long>(L.words()) + 2 * L.KP +
+           route_tiles(words) * kRouteStride + slow_words(words);
 }
 
 }  // namespace
@@ -42,9 +53,9 @@ long long ctx_stride(const qi_plan* p, long long words)
 {
     if (!use_matrix(p, words))
         return ntt_ctx_words(p);
-    const MatLayout L = ctx_layout(p);
-    return static_cast<long long>(L.words()) + 2 * L.KP +
-           route_tiles(words) * kRouteStride + slow_words(words);
+    // 256 < k <= 384: the NTT engine's context follows the matrix one, for
+    // rows the matrix cores cannot address (matrix_cores_take)
+    return mat_ctx_words(p, words) + (p->mbig ? ntt_ctx_words(p) : 0);
 }
 
 // the slow-tile lists of n contexts (behind each route table)
@@ -71,6 +82,13 @@ int build_ctx(qi_plan* p, const uint16_t* d_ids, int n_stripes, const Oor* in,
     if (!use_matrix(p, words))
         return ntt_build_ctx(p, d_ids, n_stripes, static_cast<int32_t*>(d_ctx), cs, s);
     const MatLayout L = ctx_layout(p);
+    if (p->mbig) {
+        const int rc = ntt_build_ctx(p, d_ids, n_stripes,
+                                     static_cast<int32_t*>(d_ctx) + mat_ctx_words(p, words), cs,
+                                     s);
+        if (rc)
+            return rc;
+    }
     return launch_decode_ctx(p->k, p->n, p->r, p->sys ? 1 : 0, L, d_ids, n_stripes,
                              static_cast<int32_t*>(d_ctx), cs, in, slot_base, by_pos,
                              words, p->d_err, s);
@@ -101,14 +119,17 @@ int qi_gpu_encode(qi_plan* p, const uint16_t* d_data, long long dss,
         return 0;
     Oor oor{d_counts, d_entries, p->n_outputs, cap};
     RowDst out{d_out, oss, ors};
-    if (!use_matrix(p, words))
+    RowSrc src{d_data, dss, drs, 1 << 30, nullptr, 0, 0, 0, p->k, 0};
+    // k > 256: the NTT engine, unless the matrix cores take the batch (mbig
+    // plans with a generator, whole tiles, addressable rows)
+    if (p->ntt && !(p->d_gen && use_matrix(p, words) &&
+                    matrix_cores_take(src, out, p->gen.R, words)))
         return ntt_encode(p, d_data, dss, drs, out, words, n_stripes,
                           d_counts ? &oor : nullptr, st(stream));
     if (!p->d_gen)
         return launch_encode_fnt(p->k, p->n, p->n_outputs, p->d_twist, d_data,
                                  dss, drs, out, words, n_stripes, oor,
                                  p->d_err, st(stream));
-    RowSrc src{d_data, dss, drs, 1 << 30, nullptr, 0, 0, 0, p->k, 0};
     return launch_matrix(p->gen, p->d_gen, 0, nullptr, 0, src, out, words,
                          n_stripes, nullptr, 0, d_counts ? &oor : nullptr, p->d_rowmap,
                          nullptr, 0, SlowList{nullptr, 0}, p->d_err, st(stream));
@@ -119,8 +140,13 @@ size_t qi_gpu_decode_ctx_bytes(const qi_plan* p, int n_stripes,
 {
     if (!p || n_stripes < 0 || words < 0)
         return 0;
-    return static_cast<size_t>(ctx_stride(p, words)) * sizeof(int32_t) *
-           static_cast<size_t>(n_stripes);
+    // an upper bound for every width up to `words` (the format, and so the
+    // stride, of a 256 < k <= 384 context depends on the width: a caller
+    // sizing for its widest batch may build narrower ones in the buffer)
+    long long w = ctx_stride(p, words);
+    if (p->mbig && words >= kRouteTile)
+        w = std::max(w, ctx_stride(p, words / kRouteTile * kRouteTile));
+    return static_cast<size_t>(w) * sizeof(int32_t) * static_cast<size_t>(n_stripes);
 }
 
 int qi_gpu_decode_ctx(qi_plan* p, const uint16_t* d_ids, const uint16_t* h_ids,
@@ -164,6 +190,10 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
     if (!use_matrix(p, words))
         return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, p->sys ? p->k : 0, out,
                           words, n_stripes, st(stream));
+    if (p->mbig && !matrix_cores_take(src, out, L.R, words))
+        return ntt_decode(p, ctx + mat_ctx_words(p, words), cs, src,
+                          d_counts ? &in : nullptr, p->sys ? p->k : 0, out, words, n_stripes,
+                          st(stream));
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, p->sys ? p->k : 0,
                          nullptr, p->d_rowid,
@@ -205,6 +235,9 @@ int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
     if (!use_matrix(p, words))
         return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, 0, out, words,
                           n_stripes, st(stream));
+    if (p->mbig && !matrix_cores_take(src, out, L.R, words))
+        return ntt_decode(p, ctx + mat_ctx_words(p, words), cs, src, d_counts ? &in : nullptr,
+                          0, out, words, n_stripes, st(stream));
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, 0, nullptr, p->d_rowid,
                          reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),
@@ -218,20 +251,22 @@ const char* qi_gpu_kernels(const qi_plan* p, long long words)
         return "";
     std::string enc, dec;
     if (!use_matrix(p, words)) {
-        enc = ntt_engine_name(p);
-        dec = std::string("ntt_ctx_kernel + ") + ntt_engine_name(p);
+        enc = ntt_kernel_names(p, false);
+        dec = "ntt_ctx_kernel + " + ntt_kernel_names(p, true);
     } else {
-        if (!p->d_gen) {
-            enc = "encode_fnt_kernel<" + std::to_string(p->K) + "," +
-                  std::to_string(p->K <= 16 ? 2 : 1) + ">";
-        } else {
-            enc = matrix_kernel_names(p->gen, words, false);
-        }
+        if (p->ntt && !p->d_gen)
+            enc = ntt_kernel_names(p, false);
+        else if (!p->d_gen)
+            enc = encode_fnt_kernel_name(p->k);
+        else
+            enc = matrix_kernel_names(p->gen, words, false, false);
         const MatLayout L = ctx_layout(p);
-        dec = std::string(p->k > 128 ? "decode_ctx_kernel<1024,true>"
-                          : p->k > 32 ? "decode_ctx_kernel<256,false>"
-                                      : "decode_ctx_kernel<64,false>") +
-              " + " + matrix_kernel_names(L, words, true);
+        // launch_decode_ctx's choice (ctx.hip)
+        dec = std::string(p->mbig ? "ntt_ctx_kernel + " : "") +
+              (p->k > 128  ? "decode_ctx_kernel<1024, true>"
+               : p->k > 32 ? "decode_ctx_lds_kernel<256>"
+                           : "decode_ctx_lds_kernel<128>") +
+              " + " + matrix_kernel_names(L, words, true, p->sys != 0);
     }
     names = "encode=" + enc + "; decode=" + dec;
     return names.c_str();

@@ -124,9 +124,16 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
 
 // matrix kernel instantiation choice
 int matrix_kp(int kin);
+// whether launch_matrix runs these rows on the matrix cores (whole
+// kRouteTile tiles): 8-byte aligned rows inside 31-bit buffer ranges.  The
+// kin > 256 layouts have no other kernel, so their callers check this first.
+bool matrix_cores_take(const RowSrc& src, const RowDst& dst, int R, long long words);
 // names of the kernels launch_matrix runs for L over `words` columns
-// (aligned rows; diagnostics: qi_gpu_kernels)
-std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor);
+// (aligned rows; diagnostics: qi_gpu_kernels); two: rows from two source
+// regions (the systematic decode)
+std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor, bool two);
+// the register-codelet encode kernel launch_encode_fnt runs (aligned rows)
+std::string encode_fnt_kernel_name(int k);
 
 // ---- host math (plan.cpp) ----
 // Lagrange matrix for points x_i = r^{ids[i]}:

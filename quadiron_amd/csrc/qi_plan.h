@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "qi_internal.h"
 
 namespace qi {
@@ -96,8 +98,9 @@ struct qi_plan {
 namespace qi {
 // ---- general-k path (ntt.hip) ----
 int ntt_plan_init(qi_plan* p);
-// "ntt_lds_kernel" (max(n, len_2k) <= 2048) or the multi-pass engine
-const char* ntt_engine_name(const qi_plan* p);
+// the NTT engine's kernels for an encode or a decode: ntt_lds_kernel<TWG>
+// (max(n, len_2k) <= 2048) or the multi-pass engine
+std::string ntt_kernel_names(const qi_plan* p, bool decode);
 void ntt_plan_free(qi_plan* p);
 long long ntt_ctx_words(const qi_plan* p);
 int ntt_build_ctx(const qi_plan* p, const uint16_t* d_ids, int n_stripes, int32_t* d_ctx,

@@ -137,11 +137,17 @@ def test_cabi_errors(hip_lib):
 _craft = craft_oor_columns
 
 
-def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
+def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True,
+                     encoder=None, oracle_stripes=None, windows=None):
+    """Encode S random stripes, decode each from its own random k-subset,
+    through both decode layouts.  check_oracle: the first 3 stripes' outputs
+    and OOR lists bit-exact against the oracle; oracle_stripes + windows:
+    those stripes' outputs, OOR lists and decodes against the oracle column
+    window by column window (full-size batches)."""
     torch = _torch()
     import quadiron_amd as qa
     rng = np.random.default_rng(seed)
-    plan = qa.Plan(k, m, sys_)
+    plan = qa.Plan(k, m, sys_, encoder=encoder)
     no = plan.n_outputs
     data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
     for s in range(min(S, 2)):
@@ -184,7 +190,18 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True):
                       entries=entries, cap=cap)
     torch.cuda.synchronize()
     assert err == 0
-    assert (dec.cpu().numpy().view(np.uint16) == data).all()
+    dec_h = dec.cpu().numpy().view(np.uint16)
+    assert (dec_h == data).all()
+    for s in oracle_stripes or ():
+        ent_s = ent_h[s].copy()
+        for i in range(no):  # the buckets are unordered; the oracle's ascend
+            ent_s[i, :cnt_h[s, i]].sort()
+        missing = np.ones(k + m, np.int32)
+        missing[ids[s].astype(np.int64)] = 0
+        check_windows_vs_oracle(
+            k, m, sys_, data[s].view(np.uint8).reshape(k, 2 * P),
+            out_h[s].view(np.uint8).reshape(no, 2 * P), ent_s, cnt_h[s],
+            windows, missing, dec_h[s].view(np.uint8).reshape(k, 2 * P))
 
     # the packed staging layout (qi_gpu_decode_packed): received rows back
     # to back in id order, OOR buckets by position
@@ -338,37 +355,58 @@ def test_general_path_slicing(k, m, sys_, S, P, stripes):
     (33, 31, 2, 2048),        # KS = 4 with padded inputs (x64 MFMA, zero K halves)
     (64, 960, 2, 2048),       # cfg3 generator, row blocks split over waves
 ])
-def test_matrix_encode_knob_vs_oracle(monkeypatch, k, m, S, P):
-    """QI_ENC_MATRIX=1 (read at plan creation) sends non-systematic encodes
-    through the matrix-core kernel (the default at K = 64 only): bit-exact
-    on every generator shape, including the permuted rows of the cfg3
-    Vandermonde generator."""
-    monkeypatch.setenv("QI_ENC_MATRIX", "1")
-    _batch_roundtrip(k, m, 0, S, P, seed=7 * k + m + P, n_craft=16)
+def test_matrix_encode_flag_vs_oracle(k, m, S, P):
+    """QI_PLAN_ENC_MATRIX sends non-systematic encodes through the
+    matrix-core kernel (the default at K = 64 only): bit-exact on every
+    generator shape, including the permuted rows of the cfg3 Vandermonde
+    generator."""
+    _batch_roundtrip(k, m, 0, S, P, seed=7 * k + m + P, n_craft=16, encoder="matrix")
 
 
 @pytest.mark.parametrize("k,m,S,P", [
     (64, 960, 2, 2048),       # cfg3 shape: the 64-point codelet kernel
     (33, 31, 2, 513),
 ])
-def test_codelet_encode_knob_vs_oracle(monkeypatch, k, m, S, P):
-    """QI_ENC_MATRIX=0 keeps the register FNT codelets at K = 64 too."""
-    monkeypatch.setenv("QI_ENC_MATRIX", "0")
-    _batch_roundtrip(k, m, 0, S, P, seed=11 * k + m + P, n_craft=16)
+def test_codelet_encode_flag_vs_oracle(k, m, S, P):
+    """QI_PLAN_ENC_CODELETS keeps the register FNT codelets at K = 64 too."""
+    _batch_roundtrip(k, m, 0, S, P, seed=11 * k + m + P, n_craft=16,
+                     encoder="codelets")
+
+
+def _spread(S, step=8):
+    """First, last and every `step`-th stripe of a batch."""
+    return sorted(set(range(0, S, step)) | {S - 1})
 
 
 def test_cfg2_full_size_roundtrip():
     """BASELINE cfg2 geometry (k=16, n=64, 64 KiB packets) at 32 stripes:
-    encode -> per-stripe random erasures -> decode == data, and stripe 0
-    bit-exact against the oracle."""
-    _batch_roundtrip(16, 48, 0, 32, 32768, seed=2, n_craft=8,
-                     check_oracle=True)
+    encode -> per-stripe random erasures -> decode == data; stripes 0-2
+    bit-exact against the oracle over the whole block, and the first, last
+    and every 8th stripe by column windows (start, middle, end) with their
+    OOR lists and decodes."""
+    P = 32768
+    _batch_roundtrip(16, 48, 0, 32, P, seed=2, n_craft=8, check_oracle=True,
+                     oracle_stripes=_spread(32),
+                     windows=[(0, 512), (P // 2 - 256, P // 2 + 256), (P - 512, P)])
 
 
 def test_cfg4_all_patterns_distinct():
-    """cfg4: per-stripe n-k random erasures (every stripe its own context)."""
-    _batch_roundtrip(16, 48, 0, 256, 2048, seed=4, n_craft=0,
-                     check_oracle=False)
+    """cfg4: per-stripe n-k random erasures (every stripe its own context);
+    the first, last and every 8th stripe's outputs, OOR lists and decodes
+    against the oracle over the whole block."""
+    P = 2048
+    _batch_roundtrip(16, 48, 0, 256, P, seed=4, n_craft=0, check_oracle=False,
+                     oracle_stripes=_spread(256), windows=[(0, P)])
+
+
+def test_cfg3_random_patterns_vs_oracle():
+    """cfg3 geometry (k=64, n=1024, 4 KiB packets) at 96 stripes, each
+    decoded from its own random 64-subset of the 1024 fragments: the first,
+    last and every 8th stripe against the oracle by column windows."""
+    P = 2048
+    _batch_roundtrip(64, 960, 0, 96, P, seed=6, n_craft=0, check_oracle=False,
+                     oracle_stripes=_spread(96),
+                     windows=[(0, 256), (1024 - 128, 1024 + 128), (P - 256, P)])
 
 
 @pytest.mark.parametrize("k,m,S,P", [
@@ -383,6 +421,93 @@ def test_decode_row_scales_many_stripes(k, m, S, P):
     32640) are rescaled by a unit s on the GPU (pack_row's search); every
     stripe must still decode back to its data."""
     _batch_roundtrip(k, m, 0, S, P, seed=3 * k + S, n_craft=0, check_oracle=False)
+
+
+@pytest.mark.parametrize("sys_", [0, 1])
+def test_big_matrix_path_unaligned_rows(sys_):
+    """256 < k <= 384 at a whole-tile width (1024 columns) but with rows the
+    matrix cores cannot address (base offset by one u16, odd row strides):
+    the encode runs the NTT engine and the decode uses the NTT context that
+    follows the matrix one (these calls used to fail with -3)."""
+    torch = _torch()
+    import quadiron_amd as qa
+    k, m, S, P = 300, 100, 2, 1024
+    rng = np.random.default_rng(300 + sys_)
+    plan = qa.Plan(k, m, sys_)
+    no = plan.n_outputs
+    data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
+    _craft(k, m, sys_, data[0], rng, 8)
+    dbig = torch.zeros((S, k, P + 1), dtype=torch.int16, device="cuda")
+    dd = dbig[:, :, 1:]
+    dd.copy_(torch.from_numpy(data.view(np.int16)))
+    obig = torch.zeros((S, no, P + 3), dtype=torch.int16, device="cuda")
+    out = obig[:, :, 3:]
+    cap = 64
+    counts = torch.zeros(S * no, dtype=torch.int32, device="cuda")
+    entries = torch.zeros(S * no * cap, dtype=torch.int32, device="cuda")
+    plan.encode(dd, out, counts, entries, cap)
+    torch.cuda.synchronize()
+    out_h = out.cpu().numpy().view(np.uint16)
+    cnt_h = counts.cpu().numpy().view(np.uint32).reshape(S, no)
+    ent_h = entries.cpu().numpy().view(np.uint32).reshape(S, no, cap)
+    o_out, o_oor, o_cnt = oracle_encode_blocks(
+        k, m, sys_, data[0].view(np.uint8).reshape(k, 2 * P), cap)
+    assert (out_h[0].view(np.uint8).reshape(no, 2 * P) == o_out).all()
+    assert (cnt_h[0] == o_cnt).all() and cnt_h[0].sum() > 0
+    for i in range(no):
+        assert (np.sort(ent_h[0, i, :cnt_h[0, i]]) == o_oor[i, :o_cnt[i]]).all()
+    ids = np.stack([np.sort(rng.choice(k + m, k, replace=False)) for _ in range(S)])
+    ids = ids.astype(np.uint16)
+    di = torch.from_numpy(ids.view(np.int16)).cuda()
+    ctx = torch.randint(0, 256, (plan.ctx_bytes(S, P),), dtype=torch.uint8,
+                        device="cuda")
+    plan.decode_ctx(di, ctx, P, counts, entries, cap)
+    decbig = torch.zeros((S, k, P + 1), dtype=torch.int16, device="cuda")
+    dec = decbig[:, :, 1:]
+    assert plan.decode(ctx, di, out, dec, data=dd, counts=counts, entries=entries,
+                       cap=cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec, dd)
+    # the same contexts with aligned copies of the rows: the matrix cores
+    out2 = out.contiguous()
+    dec2 = torch.zeros((S, k, P), dtype=torch.int16, device="cuda")
+    assert plan.decode(ctx, di, out2, dec2, data=dd.contiguous(), counts=counts,
+                       entries=entries, cap=cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec2, dd)
+
+
+def test_big_matrix_ctx_sized_for_a_wider_batch():
+    """A context buffer sized for the widest batch (ragged: NTT format) holds
+    the contexts of a narrower whole-tile batch (matrix format, larger): the
+    size query is a bound over every width up to the one asked (ADVICE r3:
+    the matrix context overflowed the buffer).  Guard bytes behind the
+    buffer must stay untouched."""
+    torch = _torch()
+    import quadiron_amd as qa
+    k, m, S, Pmax, P = 300, 212, 2, 1500, 1024
+    plan = qa.Plan(k, m, False)
+    assert plan.ctx_bytes(S, Pmax) >= plan.ctx_bytes(S, P)
+    rng = np.random.default_rng(17)
+    data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
+    dd = torch.from_numpy(data.view(np.int16)).cuda()
+    out = torch.zeros((S, plan.n_outputs, P), dtype=torch.int16, device="cuda")
+    cap = 64
+    counts = torch.zeros(S * plan.n_outputs, dtype=torch.int32, device="cuda")
+    entries = torch.zeros(S * plan.n_outputs * cap, dtype=torch.int32, device="cuda")
+    plan.encode(dd, out, counts, entries, cap)
+    ids = np.stack([np.sort(rng.choice(k + m, k, replace=False))
+                    for _ in range(S)]).astype(np.uint16)
+    di = torch.from_numpy(ids.view(np.int16)).cuda()
+    nb = plan.ctx_bytes(S, Pmax)
+    buf = torch.full((nb + 4096,), 0x5A, dtype=torch.uint8, device="cuda")
+    plan.decode_ctx(di, buf[:nb], P, counts, entries, cap)
+    dec = torch.zeros_like(dd)
+    assert plan.decode(buf[:nb], di, out, dec, counts=counts, entries=entries,
+                       cap=cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec, dd)
+    assert bool((buf[nb:] == 0x5A).all())
 
 
 def test_empty_and_tiny_blocks(hip_lib):
