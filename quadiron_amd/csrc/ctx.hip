@@ -8,29 +8,6 @@
 #include "matrix_pack.h"
 #include "qi_internal.h"
 
-// timing probes only (QI_PROBE_SKIP bits skip context phases; results wrong)
-#ifndef QI_PROBE_SKIP
-#define QI_PROBE_SKIP 0
-#endif
-
-// timestamp probe (QI_PROBE_TS builds only): per workgroup, s_memrealtime
-// (100 MHz) at the phase boundaries of decode_ctx_lds_kernel, read back by
-// qi_probe_read (tools/ctx_ts.py)
-#ifdef QI_PROBE_TS
-__device__ unsigned long long qi_probe_ts[8192][8];
-extern "C" int qi_probe_read(void* host, size_t bytes)
-{
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(qi_probe_ts), bytes) == hipSuccess ? 0 : -1;
-}
-#define QI_TS(n)                                                                    \
-    do {                                                                            \
-        if (threadIdx.x == 0)                                                       \
-            qi_probe_ts[blockIdx.x & 8191][n] = __builtin_amdgcn_s_memrealtime();   \
-    } while (0)
-#else
-#define QI_TS(n) ((void)0)
-#endif
-
 namespace qi {
 // ---------------------------------------------------------------------------
 // Per-stripe decode context: the Lagrange form of DecodeContext::init
@@ -190,15 +167,9 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
         const uint32_t odd = __shfl_xor(v[m], 1, lpr);
         if (i < kin) {
             row[i] = v[m];
-#ifndef QI_PROBE_NOPLAIN
             plain[static_cast<size_t>(t) * kin + i] = static_cast<int32_t>(v[m]);
-#endif
             sum += v[m];
-#ifndef QI_PROBE_NOPACKED
             if (!(sub & 1)) {
-#else
-            if (false) {
-#endif
                 const int32_t lo = balanced(v[m]);
                 const int32_t hi = i + 1 < kin ? balanced(odd) : 0;
                 packed[i >> 1] = static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xffffu) |
@@ -207,10 +178,8 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
         }
     }
     // pairs past kin up to KP stay zero (the dot2 kernel's padding)
-#ifndef QI_PROBE_NOPACKED
     for (int j = (kin + 1) / 2 + sub; j < KP; j += lpr)
         packed[j] = 0;
-#endif
     sum = grp_add(sum, lpr);
     if (sub == 0) {
         // sum mod q by two folds (2^16 = -1), then canonical
@@ -251,7 +220,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // instruction at k = 64)
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
-    QI_TS(0);
     int32_t* mat = ctx + s * ctx_stride;
     // BIG (128 < k <= 256): the k x k matrix (up to 256 KB) does not fit
     // LDS; its rows live in the context's own `plain` section (pitch k),
@@ -272,11 +240,11 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         route[ntiles * kRouteStride] = 0;
     if (tid < k) {
         const uint32_t id = ids[static_cast<long long>(s) * k + tid];
-        xs[tid] = (QI_PROBE_SKIP & 32) ? id + 2 : powm(r, id);
+        xs[tid] = powm(r, id);
         cids[tid] = static_cast<int32_t>(id);
     }
     __syncthreads();
-    if (!(QI_PROBE_SKIP & 1) && in_oor.counts && tid < k) {
+    if (in_oor.counts && tid < k) {
         const int id = ids[static_cast<long long>(s) * k + tid];
         const int slot = (by_pos ? tid : id) - slot_base;
         if (slot >= 0) {
@@ -297,7 +265,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             }
         }
     }
-    QI_TS(1);
     // A(x) = prod_i (x - x_i) on wave 0: slot u of lane d holds coefficient
     // 64 u + d (u < nslot <= 6), lazy (folded once per step, |a| < 2^17):
     // the shift by DPP (wave_shr:1) with the slot carry by readlane, the
@@ -305,7 +272,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // ds_bpermute shifts and canonical mulm of round 2 took ~620 cycles per
     // step: 62 us of a k = 200 context).  A is monic: A[k] = 1 is set
     // explicitly, so k = 64 u needs no extra slot.  Stored balanced.
-    if (!(QI_PROBE_SKIP & 2) && tid < 64) {  // wave 0 (wave-uniform)
+    if (tid < 64) {  // wave 0 (wave-uniform)
         constexpr int NS = kMatMaxKin / 64;
         const int nslot = (k + 63) / 64;
         int32_t xv[NS], au[NS];
@@ -351,8 +318,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             A[k] = 1;
     }
     __syncthreads();
-    QI_TS(2);
-    if (!(QI_PROBE_SKIP & 4) && tid < k) {
+    if (tid < k) {
         // Q_i = A / (x - x_i) by synthetic division from the top, and
         // A'(x_i) = Q_i(x_i) by Horner beside it (two interleaved chains),
         // lazy as in decode_ctx_lds_kernel (|q| < 98400, |h| < 2^18); the
@@ -407,19 +373,17 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         }
     }
     __syncthreads();
-    QI_TS(3);
     {
         // LPR lanes per row: 4 entries per lane at k = 64
         // (16 entries per lane: lpr = 32 covers k <= 512)
         const int q4 = (k + 3) / 4;
         const int lpr = q4 <= 4 ? 4 : q4 <= 8 ? 8 : q4 <= 16 ? 16 : 32;
-        for (int t = tid / lpr; !(QI_PROBE_SKIP & 8) && t < L.R; t += NT / lpr)
+        for (int t = tid / lpr; t < L.R; t += NT / lpr)
             pack_row_grp(Mt + t * kp, cinv, L, t, mat, tid & (lpr - 1), lpr);
     }
-    if (!(QI_PROBE_SKIP & 16) && L.KS()) {
+    if (L.KS()) {
         // the matrix-core operand tiles, from the row-scaled entries in LDS
         __syncthreads();
-        QI_TS(4);
         // per (row t, 4 consecutive entries): split once, then place the
         // a / b byte words in their tile dwords (pack_mf_dword's layout;
         // rows t >= R are zero).  Items run row-fastest, so 16 lanes read
@@ -490,10 +454,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             }
         }
     }
-#ifdef QI_PROBE_TS
-    __syncthreads();
-#endif
-    QI_TS(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -545,7 +505,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
     extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
-    QI_TS(0);
     int32_t* mat = ctx + s * ctx_stride;
     const int kp = ctx_pitch(k);
     uint32_t* Mt = qi_ctx_lds;
@@ -570,7 +529,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
     }
     if (tid < 64 && 64 + tid < k)
         xt1 = balanced(canon_lz(rpow_lz(rp, ids[static_cast<long long>(s) * k + 64 + tid], lgn)));
-    QI_TS(1);
     int32_t ab0 = 0;  // wave 0: balanced A[lane] (k <= 64), for the Q chains
     if (tid < 64) {
         // A(x) = prod_i (x - x_i): lane d holds coefficient d (a0) and
@@ -628,7 +586,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         }
     }
     __syncthreads();
-    QI_TS(2);
     if (tid < k) {
         // Q_i = A / (x - x_i) by synthetic division from the top, and
         // A'(x_i) = Q_i(x_i) by Horner beside it; lazy: |q| < 98400,
@@ -686,7 +643,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         }
     }
     __syncthreads();
-    QI_TS(3);
     // items: (row t, 4-entry group j), rows fastest (16 lanes = 16 rows of
     // one group: the LDS pitch 4 x odd makes their b128 reads conflict-free)
     const int KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
@@ -707,7 +663,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         *reinterpret_cast<uint4*>(Mt + t * kp + i0) = uint4{e[0], e[1], e[2], e[3]};
     }
     __syncthreads();
-    QI_TS(4);
     // per row: sum, scale test, the rare rescale (4 lanes per row, quad
     // reductions by DPP; a row needs a unit scale with probability ~5 k /
     // 65537, i.e. ~27 % of the stripes at k = 64, so the rescale runs on the
@@ -768,7 +723,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         }
     }
     __syncthreads();
-    QI_TS(5);
     // the operand tiles (pack_mf_dword's layout: [a | 0], [0 | b], [b | a];
     // the zero halves are not written at KS >= 4, the kernel never reads
     // them): items rows-fastest, so a wave's stores fill whole tile lines
@@ -836,7 +790,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
     const int pz = (k + 1) / 2, npz = L.KP - pz;
     for (int it = tid; it < L.R * npz; it += NT)
         mat[static_cast<size_t>(it / npz) * L.KP + pz + it % npz] = 0;
-    QI_TS(6);
 }
 
 int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,

@@ -26,31 +26,6 @@
 #include "matrix_pack.h"
 #include "qi_internal.h"
 
-// timestamp probe of matrix_mfma_kernel (QI_PROBE_TS builds only): per
-// block, s_memrealtime (100 MHz) at entry, after the row loads, after the
-// staging barrier and at exit, plus HW_ID / XCC_ID (tools/mm_ts.py)
-#ifdef QI_PROBE_TS
-__device__ unsigned long long qi_probe_mm[16384][6];
-extern "C" int qi_probe_mm_read(void* host, size_t bytes)
-{
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(qi_probe_mm), bytes) == hipSuccess ? 0 : -1;
-}
-#define QI_MM_TS(n)                                                                      \
-    do {                                                                                 \
-        if (threadIdx.x == 0)                                                            \
-            qi_probe_mm[blockIdx.x & 16383][n] = __builtin_amdgcn_s_memrealtime();       \
-    } while (0)
-#define QI_MM_HW()                                                                       \
-    do {                                                                                 \
-        if (threadIdx.x == 0) {                                                          \
-            qi_probe_mm[blockIdx.x & 16383][4] = __builtin_amdgcn_s_getreg(4 | (31 << 11)); \
-            qi_probe_mm[blockIdx.x & 16383][5] = __builtin_amdgcn_s_getreg(20 | (31 << 11)); \
-        }                                                                                \
-    } while (0)
-#else
-#define QI_MM_TS(n) ((void)0)
-#define QI_MM_HW() ((void)0)
-#endif
 
 namespace qi {
 
@@ -711,6 +686,35 @@ __device__ __forceinline__ void stage_route_marks(const uint32_t* rm, int n_rm,
     }
 }
 
+// The same from the route-table entry rt (count + kRouteCap entries) read
+// by scalar loads (constant address space): a vector load here is ordered
+// with the kernel's streaming stores and its row prefetch in vmcnt, so
+// waiting for it drained both every tile.  Returns the count, or -1 when the
+// tile overflowed the table (scan the buckets).
+__device__ __forceinline__ int stage_route_marks_s(const uint32_t* rt, long long col0, int* s_i,
+                                                   uint32_t* s_col)
+{
+    using CU = const __attribute__((address_space(4))) uint32_t;
+    CU* c = (CU*)rt;
+    uint32_t e[kRouteStride];
+#pragma unroll
+    for (int i = 0; i < kRouteStride; i++)
+        e[i] = c[i];
+    const uint32_t rc = e[0];
+    if (rc > static_cast<uint32_t>(kRouteCap))
+        return -1;
+    const int tid = static_cast<int>(threadIdx.x);
+    if (tid < static_cast<int>(rc)) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < kRouteCap; i++)
+            v = tid == i ? e[1 + i] : v;
+        s_i[tid] = static_cast<int>(v >> 16);
+        s_col[tid] = static_cast<uint32_t>(col0 / kRouteTile * kRouteTile + (v & 0xffffu));
+    }
+    return static_cast<int>(rc);
+}
+
 // block-wide scan of the buckets into the LDS list (s_i, s_col) of the
 // marks inside columns [col0, col1); returns the number of marks found
 // (> kMaxTileOor: the list is incomplete, use the slow path)
@@ -1107,8 +1111,6 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     uint32_t* s_col = reinterpret_cast<uint32_t*>(s_i + kMaxTileOor);
     int* s_cnt = reinterpret_cast<int*>(s_col + kMaxTileOor);
 
-    QI_MM_TS(0);
-    QI_MM_HW();
     int s, tile;
     block_map(blockIdx.x, tiles, s, tile);
     const int kin = L.kin;
@@ -1247,17 +1249,6 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             ld_dw<CPL / 2, true, kAuxLd>(g, off, voff, w[r]);
         }
     }
-#ifdef QI_PROBE_TS
-    {
-        uint32_t dep = 0;
-#pragma unroll
-        for (int r = 0; r < KH / RG; r++)
-            dep |= w[r][0];
-        if (dep == 0x12345678u)
-            qi_probe_mm[0][0] = 0;
-    }
-    QI_MM_TS(1);
-#endif
     const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) +
                           4 * ((cl % 64) / 16) + cl % 4;
 #pragma unroll
@@ -1295,7 +1286,6 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
         __syncthreads();
         n_lm = n_rm;
     }
-    QI_MM_TS(2);
 
     // matrix cores: wave wv covers nst super tiles of 64 columns, for each
     // block of 16 output rows in turn (the next block's operands prefetched)
@@ -1548,10 +1538,6 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             rb_body(rb + rbs, bB, ktB, rsB, prB);
         }
     }
-#ifdef QI_PROBE_TS
-    __syncthreads();
-#endif
-    QI_MM_TS(3);
     if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
         push_slow_tile(slow, s, col0, NCOL);
 }
@@ -1579,6 +1565,38 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
 // The arithmetic, operand tiles, epilogue and OOR handling are
 // matrix_mfma_kernel's (byte split, 2^16 = -1, D2 folded first at KS = 16).
 // ---------------------------------------------------------------------------
+// Coefficient M[t][pos] of this lane's output row t (lane (g, t & 15) of a
+// 16-row block) from the block's [b | a] operand tile, held in registers as
+// KS / 2 v4i (x64 pairs; lane 16 g + t, dword 2 ks + dw: bytes K = 32 ks +
+// 8 g + 4 dw + 0..3, b at K = pos and a at K = 16 KS + pos): the row-scaled
+// entry as 256 a + b (balanced), the value the `plain` section holds.  pos is
+// wave-uniform; the two dwords come from the lane holding them by
+// ds_bpermute.
+template <int NP>
+__device__ __forceinline__ int32_t pick_dw(const qi_v4i (&v)[NP], int idx)
+{
+    int32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < NP; i++)
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+            r = idx == 4 * i + e ? v[i][e] : r;
+    return r;
+}
+
+template <int NP>
+__device__ __forceinline__ int32_t coef_from_tiles(const qi_v4i (&b2)[NP], int pos, int lane)
+{
+    constexpr int KS = 2 * NP;
+    const int ks = pos >> 5, g = (pos & 31) >> 3, dw = (pos >> 2) & 1, sh = 8 * (pos & 3);
+    const int32_t vb = pick_dw(b2, 2 * ks + dw);
+    const int32_t va = pick_dw(b2, 2 * (ks + KS / 2) + dw);
+    const int src = 16 * g + (lane & 15);
+    const int32_t xb = __shfl(vb, src), xa = __shfl(va, src);
+    const int32_t b = (xb << (24 - sh)) >> 24, a = (xa << (24 - sh)) >> 24;
+    return 256 * a + b;
+}
+
 template <int KS, int WR>
 struct OsTile {
     static constexpr int kWaves = 8;
@@ -1715,25 +1733,37 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             off0[r] = static_cast<uint32_t>(id * src.rs0 * 2) + lane;
         }
     }
-    uint32_t w[RPT][2];
-    auto issue_rows = [&](int tile) {
-        const int so = tile * NCOL * 2;  // byte offset of the tile's first column
+    // DEEP (KS = 4, the short decodes): two tiles of rows in flight per
+    // block (two register sets) -- with one, a CU kept ~32 KB of loads in
+    // flight and the cfg3 decode was bound by the load latency
+#ifndef QI_OS_DEEP
+#define QI_OS_DEEP 1
+#endif
+    constexpr bool DEEP = QI_OS_DEEP && KS == 4;
+    uint32_t w[RPT][2], w2[DEEP ? RPT : 1][2];
+    // rows of `tile` into wr; an invalid tile (past the block's range) loads
+    // from past the buffer's extent (no memory access, zeros), so the number
+    // of loads in flight is the same on every path
+    auto issue_rows_to = [&](int tile, bool valid, auto& wr) {
+        const int so = valid ? tile * NCOL * 2 : 0;  // byte offset of the tile's first column
+        const uint32_t oob = valid ? 0u : kOob;
 #pragma unroll
         for (int r = 0; r < RPT; r++) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(g0.r, static_cast<int>(off0[r]),
-                                                                so, kAuxLdOs);
-            w[r][0] = v[0];
-            w[r][1] = v[1];
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(
+                g0.r, static_cast<int>(off0[r] | oob), so, kAuxLdOs);
+            wr[r][0] = v[0];
+            wr[r][1] = v[1];
             if constexpr (TWO) {
                 const auto u = __builtin_amdgcn_raw_buffer_load_b64(
-                    g1.r, static_cast<int>(off1[r]), so, kAuxLdOs);
-                w[r][0] |= u[0];
-                w[r][1] |= u[1];
+                    g1.r, static_cast<int>(off1[r] | oob), so, kAuxLdOs);
+                wr[r][0] |= u[0];
+                wr[r][1] |= u[1];
             }
         }
     };
+    auto issue_rows = [&](int tile) { issue_rows_to(tile, true, w); };
     const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) + 4 * ((cl % 64) / 16);
-    auto write_rows = [&](uint8_t* img) {
+    auto write_rows_from = [&](uint8_t* img, const auto& w) {
 #pragma unroll
         for (int r = 0; r < RPT; r++) {
             const int i = O::kRpp * r + rowgrp;
@@ -1743,6 +1773,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             *reinterpret_cast<uint32_t*>(img + (KH + i) * RSB + lpos) = lo;
         }
     };
+    auto write_rows = [&](uint8_t* img) { write_rows_from(img, w); };
 
     // OOR marks of the received rows in a tile (route table or bucket
     // scan) into mark list mb; returns the count (all threads)
@@ -1759,12 +1790,11 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             return 0;
         const long long col0 = static_cast<long long>(tile) * NCOL;
         if (a.route) {
-            const uint32_t* rt = a.route + s * a.rstride + (col0 / kRouteTile) * kRouteStride;
-            const uint32_t rc = rt[0];
-            if (rc <= static_cast<uint32_t>(kRouteCap)) {
-                stage_route_marks(rt + 1, static_cast<int>(rc), col0, s_i(mb), s_col(mb));
-                return static_cast<int>(rc);
-            }
+            const int rc = stage_route_marks_s(
+                a.route + s * a.rstride + (col0 / kRouteTile) * kRouteStride, col0, s_i(mb),
+                s_col(mb));
+            if (rc >= 0)
+                return rc;
         }
         OorScan sc{in_oor, sid, src.by_pos, a.slot_base, kin, s, false};
         const int cnt = scan_tile_marks(sc, col0, col0 + NCOL, a.words, s_cnt(mb), s_i(mb),
@@ -1842,7 +1872,9 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
                 continue;
             const int pos = __builtin_amdgcn_readfirstlane(mi[e]);
             const long long d = static_cast<long long>(wcu) - cb;
-            const int32_t corr = plain[tcl * kin + pos];
+            // the coefficient from the wave's own operand tiles (no memory
+            // load: waiting for one drained the stores and the prefetch)
+            const int32_t corr = coef_from_tiles(b2[j], pos, l);
 #pragma unroll
             for (int c = 0; c < 16; c++) {
                 const int32_t yc = fold(fold(y[c] - corr));
@@ -1915,6 +1947,47 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     if (t0 >= t1)
         return;
     auto img = [&](int b) { return qi_lds + b * O::kImg; };
+    if constexpr (DEEP) {
+        issue_rows_to(t0, true, w);
+        issue_rows_to(t0 + 1, t0 + 1 < t1, w2);
+        write_rows_from(img(0), w);
+        int nl[2];
+        nl[0] = stage_marks(t0, 0);
+        nl[1] = 0;
+        __syncthreads();
+        // tile's rows are in image b; wnext holds tile + 1's (in flight),
+        // wfree is free: it takes tile + 2's
+        auto body = [&](int tile, auto& wnext, auto& wfree) {
+            const int b = (tile - t0) & 1;
+            const bool more = tile + 1 < t1;  // block-uniform
+            issue_rows_to(tile + 2, tile + 2 < t1, wfree);
+            const long long col0 = static_cast<long long>(tile) * NCOL + 64 * st;
+            auto none = [] {};
+            [&]<int... J>(std::integer_sequence<int, J...>) {
+                ((act[J] ? compute(img(b), col0, nl[b], s_i(b), s_col(b),
+                                   std::integral_constant<int, J>{}, none)
+                         : idle_stores()),
+                 ...);
+            }(std::make_integer_sequence<int, RPW>{});
+            // unconditional, so every path waits for wnext's loads here (a
+            // skipped write left them pending on one path, and the compiler
+            // then drained vmcnt(0) before reusing the registers); past the
+            // last tile it writes the invalid tile's zeros into an image no
+            // wave reads again
+            write_rows_from(img(b ^ 1), wnext);
+            if (more)
+                nl[b ^ 1] = stage_marks(tile + 1, b ^ 1);
+            __syncthreads();
+        };
+#pragma unroll 1
+        for (int tile = t0; tile < t1; tile += 2) {
+            body(tile, w2, w);
+            if (tile + 1 >= t1)
+                break;
+            body(tile + 1, w, w2);
+        }
+        return;
+    }
     issue_rows(t0);
     write_rows(img(0));
     int nl[2];
