@@ -10,6 +10,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <istream>
 #include <memory>
 #include <ostream>
@@ -120,6 +121,23 @@ class RsFnt {
                         uint8_t* const* outputs, size_t words, size_t offset);
     bool select_fragments(const std::vector<int>& present,
                           std::vector<int>& ids) const;
+    // the two-slot pinned pipeline behind the stream API and the blocks
+    // wider than one chunk: read(h, pitch, cont) fills the next chunk's
+    // input rows (pitch bytes apart) and returns the bytes per row (0: no
+    // more); write(h, pitch, got, byte_offset) takes a finished chunk's
+    // output rows, in chunk order
+    using RowReader = std::function<size_t(uint8_t*, size_t, bool&)>;
+    using RowWriter = std::function<void(const uint8_t*, size_t, size_t, size_t)>;
+    void encode_pipe(const RowReader& read, const RowWriter& write,
+                     std::vector<Properties>& props);
+    void decode_pipe(const std::vector<int>& ids, const std::vector<const Properties*>& props,
+                     const RowReader& read, const RowWriter& write);
+    bool encode_blocks_pipe(const std::vector<uint8_t*>& data_bufs,
+                            const std::vector<uint8_t*>& outs, std::vector<Properties>& props,
+                            size_t words);
+    bool decode_blocks_pipe(const std::vector<int>& ids, const std::vector<const uint8_t*>& rows,
+                            const std::vector<const Properties*>& props,
+                            const std::vector<uint8_t*>& outs, size_t words);
 
     qi_plan* plan_ = nullptr;
     // pinned two-slot pipeline of the stream API, kept across calls

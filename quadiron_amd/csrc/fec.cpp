@@ -317,9 +317,11 @@ void RsFnt::encode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
         if (wanted_idxs[i])
             outs[i] = parities_bufs[i];
     Timer tm;
-    encode_columns(data_bufs.data(), outs.data(), words, parities_props, 0);
+    if (!encode_blocks_pipe(data_bufs, outs, parities_props, words)) {
+        encode_columns(data_bufs.data(), outs.data(), words, parities_props, 0);
+        n_encode_ops++;
+    }
     total_enc_usec += tm.usec();
-    n_encode_ops++;
 }
 
 bool RsFnt::select_fragments(const std::vector<int>& present,
@@ -383,9 +385,12 @@ bool RsFnt::decode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
         if (wanted_idxs[t])
             outs[t] = data_bufs[t];
     Timer tm;
-    decode_columns(ids, rows, props, outs.data(), block_size_bytes / word_size, 0);
+    const size_t words = block_size_bytes / word_size;
+    if (!decode_blocks_pipe(ids, rows, props, outs, words)) {
+        decode_columns(ids, rows, props, outs.data(), words, 0);
+        n_decode_ops++;
+    }
     total_dec_usec += tm.usec();
-    n_decode_ops++;
     return true;
 }
 
@@ -518,10 +523,32 @@ void RsFnt::encode_streams_vertical(
 {
     // src/fec_base.h:463-542: packets of buf_size bytes, zero padded tail,
     // `read_bytes` of every output written for the last packet.  Here whole
-    // chunks of packets go through a two-slot pinned pipeline.
+    // chunks of packets go through the two-slot pinned pipeline.
+    reset_stats_enc();
+    Timer tm;
+    encode_pipe(
+        [&](uint8_t* h, size_t pitch, bool& cont) {
+            return read_rows(input_data_bufs, h, pitch, cont);
+        },
+        [&](const uint8_t* hout, size_t pitch, size_t got, size_t) {
+            parallel_for(n_outputs, [&](size_t i) {
+                output_parities_bufs[i]->write(reinterpret_cast<const char*>(hout + i * pitch),
+                                               static_cast<std::streamsize>(got));
+            });
+        },
+        output_parities_props);
+    total_enc_usec += tm.usec();
+}
+
+void RsFnt::encode_pipe(const RowReader& read, const RowWriter& write,
+                        std::vector<Properties>& output_parities_props)
+{
+    // chunks of whole packets alternate between two slots (pinned staging,
+    // device buffers, a HIP stream each): while one chunk is in H2D ->
+    // kernels -> D2H, the host fills the other slot with the next chunk and
+    // writes out the previous one
     for (auto& p : output_parities_props)
         p.clear();
-    reset_stats_enc();
     const size_t CH = chunk_bytes(buf_size);  // a multiple of 128 bytes
     const size_t P = CH / 2, k = n_data, no = n_outputs;
     const uint32_t cap = static_cast<uint32_t>(64 + P / 512);
@@ -531,7 +558,6 @@ void RsFnt::encode_streams_vertical(
     if (!pipe_)
         pipe_.reset(new StreamPipe);
     StreamSlot* slot = pipe_->slot;
-    Timer tm;
     auto finish = [&](StreamSlot& sl) {
         check(hipStreamSynchronize(sl.st), "sync");
         sl.busy = false;
@@ -558,10 +584,7 @@ void RsFnt::encode_streams_vertical(
                     output_parities_props[i].add(sl.offset + e, OOR_MARK);
             }
         }
-        parallel_for(no, [&](size_t i) {
-            output_parities_bufs[i]->write(reinterpret_cast<const char*>(hout + i * CH),
-                                           static_cast<std::streamsize>(sl.got));
-        });
+        write(hout, CH, sl.got, 2 * sl.offset);
     };
     size_t offset = 0;
     unsigned it = 0;
@@ -571,7 +594,7 @@ void RsFnt::encode_streams_vertical(
         if (sl.busy)
             finish(sl);
         uint8_t* h = sl.pinned(in_b + out_b + cnt_b + ent_b);
-        const size_t got = read_rows(input_data_bufs, h, CH, cont);
+        const size_t got = read(h, CH, cont);
         if (got == 0)
             break;
         const size_t words = (got + 1) / 2;
@@ -605,7 +628,6 @@ void RsFnt::encode_streams_vertical(
         finish(slot[it & 1]);
     if (slot[(it + 1) & 1].busy)
         finish(slot[(it + 1) & 1]);
-    total_enc_usec += tm.usec();
 }
 
 bool RsFnt::decode_streams_vertical(
@@ -614,8 +636,8 @@ bool RsFnt::decode_streams_vertical(
     std::vector<Properties>& input_parities_props,
     std::vector<std::ostream*>& output_data_bufs)
 {
-    // src/fec_base.h:898-1048, through the same two-slot pipeline: the k
-    // received rows of a chunk are staged back to back (packed decode)
+    // src/fec_base.h:898-1048, through the two-slot pipeline: the k received
+    // rows of a chunk are staged back to back (packed decode)
     const bool sys = type == FecType::SYSTEMATIC;
     std::vector<int> present(code_len, 0);
     if (sys)
@@ -638,8 +660,7 @@ bool RsFnt::decode_streams_vertical(
     reset_stats_dec();
     const size_t k = n_data;
     std::vector<std::istream*> src(k);
-    // OOR marks of each received row (ascending), consumed chunk by chunk
-    std::vector<std::vector<size_t>> marks(k);
+    std::vector<const Properties*> props(k, nullptr);
     for (size_t i = 0; i < k; i++) {
         const int id = ids[i];
         if (sys && id < static_cast<int>(n_data)) {
@@ -647,30 +668,47 @@ bool RsFnt::decode_streams_vertical(
         } else {
             const int s_ = sys ? id - static_cast<int>(n_data) : id;
             src[i] = input_parities_bufs[s_];
-            for (auto const& it : input_parities_props[s_].get_map())
-                marks[i].push_back(it.first);
+            props[i] = &input_parities_props[s_];
         }
     }
+    Timer tm;
+    decode_pipe(
+        ids, props,
+        [&](uint8_t* h, size_t pitch, bool& cont) { return read_rows(src, h, pitch, cont); },
+        [&](const uint8_t* hout, size_t pitch, size_t got, size_t) {
+            parallel_for(k, [&](size_t i) {
+                if (output_data_bufs[i])
+                    output_data_bufs[i]->write(reinterpret_cast<const char*>(hout + i * pitch),
+                                               static_cast<std::streamsize>(got));
+            });
+        });
+    total_dec_usec += tm.usec();
+    return true;
+}
+
+void RsFnt::decode_pipe(const std::vector<int>& ids, const std::vector<const Properties*>& props,
+                        const RowReader& read, const RowWriter& write)
+{
+    const size_t k = n_data;
+    // OOR marks of each received row (ascending), consumed chunk by chunk
+    std::vector<std::vector<size_t>> marks(k);
+    for (size_t i = 0; i < k; i++)
+        if (props[i])
+            for (auto const& it : props[i]->get_map())
+                marks[i].push_back(it.first);
     std::vector<size_t> mpos(k, 0);
     const size_t CH = chunk_bytes(buf_size);
     const size_t P = CH / 2;
     const size_t io_b = k * CH, ids_b = round64(k * 2), cnt_b = round64(k * 4);
-    const size_t ctx_b = qi_gpu_decode_ctx_bytes(plan_, 1, static_cast<long long>(P));
     if (!pipe_)
         pipe_.reset(new StreamPipe);
     StreamSlot* slot = pipe_->slot;
-    Timer tm;
     auto finish = [&](StreamSlot& sl) {
         check(hipStreamSynchronize(sl.st), "sync");
         sl.busy = false;
         if (qi_gpu_take_error(plan_))
             throw std::runtime_error("RsFnt: OOR marks lost (bucket capacity)");
-        const uint8_t* hout = sl.host + io_b;
-        parallel_for(k, [&](size_t i) {
-            if (output_data_bufs[i])
-                output_data_bufs[i]->write(reinterpret_cast<const char*>(hout + i * CH),
-                                           static_cast<std::streamsize>(sl.got));
-        });
+        write(sl.host + io_b, CH, sl.got, 2 * sl.offset);
     };
     size_t offset = 0;
     unsigned it = 0;
@@ -694,7 +732,7 @@ bool RsFnt::decode_streams_vertical(
         const size_t ent_b = round64(static_cast<size_t>(k) * cap * 4);
         const size_t small_b = ids_b + cnt_b + ent_b;
         uint8_t* h = sl.pinned(2 * io_b + small_b);
-        const size_t got = read_rows(src, h, CH, cont);
+        const size_t got = read(h, CH, cont);
         if (got == 0)
             break;
         const size_t words = (got + 1) / 2;
@@ -707,6 +745,9 @@ bool RsFnt::decode_streams_vertical(
             hcnt[i] = static_cast<uint32_t>(cm[i].size());
             std::copy(cm[i].begin(), cm[i].end(), hent + i * cap);
         }
+        // the context's size follows this chunk's width (a 256 < k <= 384
+        // context is larger at whole-tile widths than at ragged ones)
+        const size_t ctx_b = qi_gpu_decode_ctx_bytes(plan_, 1, static_cast<long long>(words));
         sl.dev(sl.in, io_b);
         sl.dev(sl.out, io_b);
         sl.dev(sl.small, small_b);
@@ -743,7 +784,70 @@ bool RsFnt::decode_streams_vertical(
         finish(slot[it & 1]);
     if (slot[(it + 1) & 1].busy)
         finish(slot[(it + 1) & 1]);
-    total_dec_usec += tm.usec();
+}
+
+// Blocks wider than one pipeline chunk (quadiron_fnt32_encode / _decode on
+// multi-MiB fragments) go through the same two-slot pinned pipeline as the
+// streams: the caller's rows are copied chunk by chunk into pinned staging
+// (parallel over the fragments) while the previous chunk is on the device,
+// so H2D, kernels, D2H and the host copies overlap.  Returns false for
+// blocks of one chunk or less (one synchronous device call).
+bool RsFnt::encode_blocks_pipe(const std::vector<uint8_t*>& data_bufs,
+                               const std::vector<uint8_t*>& outs,
+                               std::vector<Properties>& props, size_t words)
+{
+    if (words <= chunk_bytes(buf_size) / 2)
+        return false;
+    const size_t total = 2 * words;
+    size_t pos = 0;
+    encode_pipe(
+        [&](uint8_t* h, size_t pitch, bool& cont) {
+            const size_t got = std::min(pitch, total - pos);
+            parallel_for(n_data, [&](size_t i) {
+                std::memcpy(h + i * pitch, data_bufs[i] + pos, got);
+                std::memset(h + i * pitch + got, 0, pitch - got);
+            });
+            pos += got;
+            cont = pos < total;
+            return got;
+        },
+        [&](const uint8_t* hout, size_t pitch, size_t got, size_t off) {
+            parallel_for(n_outputs, [&](size_t i) {
+                if (outs[i])
+                    std::memcpy(outs[i] + off, hout + i * pitch, got);
+            });
+        },
+        props);
+    return true;
+}
+
+bool RsFnt::decode_blocks_pipe(const std::vector<int>& ids,
+                               const std::vector<const uint8_t*>& rows,
+                               const std::vector<const Properties*>& props,
+                               const std::vector<uint8_t*>& outs, size_t words)
+{
+    if (words <= chunk_bytes(buf_size) / 2)
+        return false;
+    const size_t total = 2 * words;
+    size_t pos = 0;
+    decode_pipe(
+        ids, props,
+        [&](uint8_t* h, size_t pitch, bool& cont) {
+            const size_t got = std::min(pitch, total - pos);
+            parallel_for(n_data, [&](size_t i) {
+                std::memcpy(h + i * pitch, rows[i] + pos, got);
+                std::memset(h + i * pitch + got, 0, pitch - got);
+            });
+            pos += got;
+            cont = pos < total;
+            return got;
+        },
+        [&](const uint8_t* hout, size_t pitch, size_t got, size_t off) {
+            parallel_for(n_data, [&](size_t i) {
+                if (outs[i])
+                    std::memcpy(outs[i] + off, hout + i * pitch, got);
+            });
+        });
     return true;
 }
 

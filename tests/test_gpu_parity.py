@@ -102,6 +102,59 @@ def test_cabi_vs_reference_golden(hip_lib, name):
         assert ((D + P)[dest] == g["reconstructed"][t]).all()
 
 
+@pytest.mark.parametrize("k,m,sys_", [(4, 4, 0), (6, 3, 1)])
+def test_cabi_multi_chunk_block_vs_oracle(hip_lib, k, m, sys_):
+    """quadiron_fnt32_encode / _decode on a block wider than one pipeline
+    chunk (4 MiB per fragment: 3 chunks, ragged last one) run the two-slot
+    pinned pipeline; every byte of every fragment -- FNT1 headers with the
+    OOR offsets included -- matches the oracle's C glue, OOR columns crafted
+    next to each chunk seam, and the decode restores the data."""
+    import quadiron_amd as qa
+    from qi_testlib import ptrs, vp
+    rng = np.random.default_rng(1000 + k)
+    words = 2 * 2**21 + 12345
+    B = 2 * words
+    lanes = rng.integers(0, 65536, (k, words), dtype=np.uint16)
+    for c0 in (0, 2**21 - 40, 2 * 2**21 - 40, words - 100):
+        _craft(k, m, sys_, lanes, rng, 3, col_range=(c0, min(words, c0 + 80)))
+    h = qa.QuadironFnt32(2, k, m, sys_)
+    md = h.metadata_size(B)
+    c = codec(k, m, sys_)
+    o = oracle()
+
+    def frags():
+        d = [np.concatenate([np.zeros(md, np.uint8), lanes[i].view(np.uint8)])
+             for i in range(k)]
+        return d, [np.zeros(md + B, np.uint8) for _ in range(m)]
+    d, p = frags()
+    wanted = np.ones(m if sys_ else k + m, np.int32)
+    assert h.encode(d, p, wanted, B) == 0
+    od, op = frags()
+    assert o.qo_fnt32_encode(C.byref(c), ptrs(od), ptrs(op),
+                             vp(np.ones(c.n_outputs, np.int32)), C.c_size_t(B)) == 0
+    for x, y in zip(d + p, od + op):
+        assert (x == y).all()
+    n_marks = sum(int.from_bytes(bytes(f[4:8]), "big") for f in p)
+    assert n_marks >= 3
+    miss = np.zeros(k + m, np.int32)  # m erasures, data fragment 0 among them
+    miss[[0] + list(rng.choice(np.arange(1, k + m), m - 1, replace=False))] = 1
+
+    def received(src_d, src_p):
+        return ([src_d[i].copy() if not miss[i] else np.zeros(md + B, np.uint8)
+                 for i in range(k)],
+                [src_p[i].copy() if not miss[k + i] else np.zeros(md + B, np.uint8)
+                 for i in range(m)])
+    D, P = received(d, p)
+    assert h.decode(D, P, miss, B) == 0
+    OD, OP = received(od, op)
+    assert o.qo_fnt32_decode(C.byref(c), ptrs(OD), ptrs(OP), vp(miss),
+                             C.c_size_t(B)) == 0
+    for x, y in zip(D, OD):
+        assert (x == y).all()
+    for i in range(k):
+        assert (D[i][md:] == lanes[i].view(np.uint8)).all()
+
+
 def test_cabi_word_size_1_rejected(hip_lib):
     import quadiron_amd as qa
     assert hip_lib.quadiron_fnt32_new(1, 3, 3, 0) is None
