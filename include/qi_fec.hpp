@@ -17,6 +17,8 @@
 #include <utility>
 #include <vector>
 
+#include <sys/types.h>
+
 struct qi_plan;
 
 namespace qi {
@@ -48,9 +50,50 @@ class Properties {
     std::vector<std::pair<size_t, uint32_t>> props;
 };
 
+namespace vec {
+
+// Containers of the horizontal API (QuadIron's vec::Vector<T> /
+// vec::Buffers<T>, src/vec_vector.h, src/vec_buffers.h, with T = uint32_t):
+// GF(65537) symbols 0 .. 65536 held in 32 bits.
+using Vector = std::vector<uint32_t>;
+
+class Buffers {
+  public:
+    Buffers(int n, size_t size)
+        : n_(n), size_(size), mem_(static_cast<size_t>(n) * size, 0u)
+    {
+    }
+    int get_n() const { return n_; }
+    size_t get_size() const { return size_; }
+    uint32_t* get(int i) { return mem_.data() + static_cast<size_t>(i) * size_; }
+    const uint32_t* get(int i) const { return mem_.data() + static_cast<size_t>(i) * size_; }
+
+  private:
+    int n_;
+    size_t size_;
+    std::vector<uint32_t> mem_;
+};
+
+}  // namespace vec
+
 namespace fec {
 
 enum class FecType { SYSTEMATIC, NON_SYSTEMATIC };
+
+// What FecCode::init_context_dec returns (src/fec_base.h:758-793,
+// src/fec_context.h:66-274): the fragment ids a decode uses.  The
+// per-pattern constants themselves are built on the device by every decode
+// call, together with that call's OOR marks (decode_prepare).
+class DecodeContext {
+  public:
+    explicit DecodeContext(const vec::Vector& ids, size_t size) : ids_(ids), size_(size) {}
+    const vec::Vector& get_fragments_id() const { return ids_; }
+    size_t get_size() const { return size_; }
+
+  private:
+    vec::Vector ids_;
+    size_t size_;
+};
 
 class RsFnt {
   public:
@@ -96,6 +139,28 @@ class RsFnt {
         std::vector<Properties>& input_parities_props,
         std::vector<std::ostream*>& output_data_bufs);
 
+    // Horizontal API (src/fec_base.h:129-178, 409-460, 740-878,
+    // src/fec_rs_fnt.h:178-270): one codeword per Vector call, get_size()
+    // codewords (columns) per Buffers call, all on the device.  As in the
+    // reference, the Vector calls use the non-systematic code of length n
+    // for both types (RsFnt::encode(Vector) is fft(output, words) then the
+    // post-process over n_outputs; decode(Vector) returns the polynomial's
+    // coefficients), and props are indexed by fragment id; the Buffers calls
+    // follow the type (systematic: m parities out, the data rows decoded)
+    // with props indexed by output / parity.  Data symbols must be < 65536
+    // (16-bit input; std::invalid_argument otherwise).
+    void encode(vec::Vector& output, std::vector<Properties>& props, off_t offset,
+                const vec::Vector& words);
+    void encode(vec::Buffers& output, std::vector<Properties>& props, off_t offset,
+                const vec::Buffers& words);
+    std::unique_ptr<DecodeContext> init_context_dec(const vec::Vector& fragments_ids,
+                                                    std::vector<Properties>& input_props,
+                                                    size_t size = 0);
+    void decode(DecodeContext& context, vec::Vector& output,
+                const std::vector<Properties>& props, off_t offset, vec::Vector& words);
+    void decode(DecodeContext& context, vec::Buffers& output,
+                const std::vector<Properties>& props, off_t offset, vec::Buffers& words);
+
     void reset_stats_enc()
     {
         n_encode_ops = 0;
@@ -110,12 +175,13 @@ class RsFnt {
     qi_plan* plan() const { return plan_; }
 
   private:
-    // device encode of `words` columns; outputs[i] NULL = not wanted
-    void encode_columns(const uint8_t* const* data, uint8_t* const* outputs,
+    // device encode of `words` columns on plan pl; outputs[i] NULL = not
+    // wanted (pl's n_outputs of them)
+    void encode_columns(qi_plan* pl, const uint8_t* const* data, uint8_t* const* outputs,
                         size_t words, std::vector<Properties>& props,
                         size_t offset);
     // device decode of `words` columns from the k selected fragments
-    void decode_columns(const std::vector<int>& ids,
+    void decode_columns(qi_plan* pl, const std::vector<int>& ids,
                         const std::vector<const uint8_t*>& rows,
                         const std::vector<const Properties*>& props,
                         uint8_t* const* outputs, size_t words, size_t offset);
@@ -139,7 +205,11 @@ class RsFnt {
                             const std::vector<const Properties*>& props,
                             const std::vector<uint8_t*>& outs, size_t words);
 
+    // the non-systematic plan of length n behind the Vector calls (created
+    // on first use)
+    qi_plan* hplan();
     qi_plan* plan_ = nullptr;
+    qi_plan* hplan_ = nullptr;
     // pinned two-slot pipeline of the stream API, kept across calls
     struct StreamPipe;
     std::unique_ptr<StreamPipe> pipe_;

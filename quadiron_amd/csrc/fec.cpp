@@ -156,7 +156,24 @@ RsFnt::RsFnt(FecType t, unsigned ws, unsigned k, unsigned m, size_t pkt)
 RsFnt::~RsFnt()
 {
     pipe_.reset();
+    qi_plan_destroy(hplan_);
     qi_plan_destroy(plan_);
+}
+
+qi_plan* RsFnt::hplan()
+{
+    if (hplan_)
+        return hplan_;
+    qi_plan* p = qi_plan_create(static_cast<int>(n_data), static_cast<int>(n - n_data), 0);
+    if (!p)
+        throw std::runtime_error("RsFnt: cannot create the GPU plan");
+    const hipError_t e = hipStreamCreateWithFlags(&p->host.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        qi_plan_destroy(p);
+        check(e, "hipStreamCreate");
+    }
+    hplan_ = p;
+    return p;
 }
 
 int RsFnt::get_n_outputs() const
@@ -166,25 +183,25 @@ int RsFnt::get_n_outputs() const
                                        : static_cast<int>(n);
 }
 
-void RsFnt::encode_columns(const uint8_t* const* data, uint8_t* const* outputs,
+void RsFnt::encode_columns(qi_plan* pl, const uint8_t* const* data, uint8_t* const* outputs,
                            size_t words, std::vector<Properties>& props,
                            size_t offset)
 {
     if (words == 0)
         return;
-    HostState& h = plan_->host;
+    HostState& h = pl->host;
     hipStream_t s = h.stream;
     const size_t P = pad_words(words);
-    const size_t no = n_outputs;
+    const size_t no = static_cast<size_t>(pl->n_outputs);
     size_t cap = 64 + words / 512;
-    check(h.in.reserve(n_data * P * 2) ? hipSuccess : hipErrorOutOfMemory,
+    check(h.in.reserve(static_cast<size_t>(pl->k) * P * 2) ? hipSuccess : hipErrorOutOfMemory,
           "alloc");
     check(h.out.reserve(no * P * 2) ? hipSuccess : hipErrorOutOfMemory, "alloc");
     check(h.counts.reserve(no * 4) ? hipSuccess : hipErrorOutOfMemory, "alloc");
     uint16_t* din = static_cast<uint16_t*>(h.in.p);
     uint16_t* dout = static_cast<uint16_t*>(h.out.p);
     uint32_t* dcnt = static_cast<uint32_t*>(h.counts.p);
-    for (unsigned t = 0; t < n_data; t++)
+    for (int t = 0; t < pl->k; t++)
         check(hipMemcpyAsync(din + t * P, data[t], words * 2,
                              hipMemcpyHostToDevice, s),
               "H2D");
@@ -193,7 +210,7 @@ void RsFnt::encode_columns(const uint8_t* const* data, uint8_t* const* outputs,
         check(h.entries.reserve(no * cap * 4) ? hipSuccess : hipErrorOutOfMemory,
               "alloc");
         check_rc(qi_gpu_oor_clear(dcnt, no, s), "oor_clear");
-        check_rc(qi_gpu_encode(plan_, din, 0, static_cast<long long>(P), dout, 0,
+        check_rc(qi_gpu_encode(pl, din, 0, static_cast<long long>(P), dout, 0,
                                static_cast<long long>(P),
                                static_cast<long long>(words), 1, dcnt,
                                static_cast<uint32_t*>(h.entries.p),
@@ -225,7 +242,7 @@ void RsFnt::encode_columns(const uint8_t* const* data, uint8_t* const* outputs,
     }
 }
 
-void RsFnt::decode_columns(const std::vector<int>& ids,
+void RsFnt::decode_columns(qi_plan* pl, const std::vector<int>& ids,
                            const std::vector<const uint8_t*>& rows,
                            const std::vector<const Properties*>& props,
                            uint8_t* const* outputs, size_t words,
@@ -233,10 +250,10 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
 {
     if (words == 0)
         return;
-    HostState& h = plan_->host;
+    HostState& h = pl->host;
     hipStream_t s = h.stream;
     const size_t P = pad_words(words);
-    const int k = static_cast<int>(n_data);
+    const int k = pl->k;
     // OOR marks of the received coded rows inside [offset, offset+words)
     std::vector<std::vector<uint32_t>> marks(k);
     size_t cap = 1;
@@ -257,7 +274,7 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
     for (int i = 0; i < k; i++)
         hids[i] = static_cast<uint16_t>(ids[i]);
     const size_t ctx_bytes =
-        qi_gpu_decode_ctx_bytes(plan_, 1, static_cast<long long>(words));
+        qi_gpu_decode_ctx_bytes(pl, 1, static_cast<long long>(words));
     const size_t cnt_off = 0, ent_off = 64 * ((k * 4 + 63) / 64);
     if (!h.in.reserve(static_cast<size_t>(k) * P * 2) ||
         !h.out.reserve(static_cast<size_t>(k) * P * 2) ||
@@ -282,11 +299,11 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
     // received rows staged by position; OOR buckets by position
     uint32_t* dcnt = reinterpret_cast<uint32_t*>(dcb + cnt_off);
     uint32_t* dent = reinterpret_cast<uint32_t*>(dcb + ent_off);
-    check_rc(qi_gpu_decode_ctx_packed(plan_, static_cast<uint16_t*>(h.ids.p), hids.data(), 1,
+    check_rc(qi_gpu_decode_ctx_packed(pl, static_cast<uint16_t*>(h.ids.p), hids.data(), 1,
                                       dcnt, dent, static_cast<int>(cap),
                                       static_cast<long long>(words), h.ctx.p, s),
              "decode context");
-    check_rc(qi_gpu_decode_packed(plan_, h.ctx.p, din, 0, static_cast<long long>(P), dcnt,
+    check_rc(qi_gpu_decode_packed(pl, h.ctx.p, din, 0, static_cast<long long>(P), dcnt,
                                   dent, static_cast<int>(cap), dout, 0,
                                   static_cast<long long>(P), static_cast<long long>(words), 1,
                                   s),
@@ -297,7 +314,7 @@ void RsFnt::decode_columns(const std::vector<int>& ids,
                                  hipMemcpyDeviceToHost, s),
                   "D2H");
     check(hipStreamSynchronize(s), "sync");
-    if (qi_gpu_take_error(plan_))
+    if (qi_gpu_take_error(pl))
         throw std::runtime_error("RsFnt: OOR marks lost (bucket capacity)");
 }
 
@@ -318,7 +335,7 @@ void RsFnt::encode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
             outs[i] = parities_bufs[i];
     Timer tm;
     if (!encode_blocks_pipe(data_bufs, outs, parities_props, words)) {
-        encode_columns(data_bufs.data(), outs.data(), words, parities_props, 0);
+        encode_columns(plan_, data_bufs.data(), outs.data(), words, parities_props, 0);
         n_encode_ops++;
     }
     total_enc_usec += tm.usec();
@@ -387,7 +404,7 @@ bool RsFnt::decode_blocks_vertical(std::vector<uint8_t*>& data_bufs,
     Timer tm;
     const size_t words = block_size_bytes / word_size;
     if (!decode_blocks_pipe(ids, rows, props, outs, words)) {
-        decode_columns(ids, rows, props, outs.data(), words, 0);
+        decode_columns(plan_, ids, rows, props, outs.data(), words, 0);
         n_decode_ops++;
     }
     total_dec_usec += tm.usec();
@@ -574,7 +591,7 @@ void RsFnt::encode_pipe(const RowReader& read, const RowWriter& write,
                 dp[i] = sl.host + i * CH;
             for (size_t i = 0; i < no; i++)
                 op[i] = hout + i * CH;
-            encode_columns(dp.data(), op.data(), words, output_parities_props,
+            encode_columns(plan_, dp.data(), op.data(), words, output_parities_props,
                            sl.offset);
         } else {
             for (size_t i = 0; i < no; i++) {
@@ -849,6 +866,213 @@ bool RsFnt::decode_blocks_pipe(const std::vector<int>& ids,
             });
         });
     return true;
+}
+
+// ---------------------------------------------------- horizontal API
+
+namespace {
+
+std::vector<unsigned> id_order(const vec::Vector& ids, unsigned k)
+{
+    std::vector<unsigned> ord(k);
+    for (unsigned i = 0; i < k; i++)
+        ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](unsigned a, unsigned b) { return ids[a] < ids[b]; });
+    for (unsigned i = 1; i < k; i++)
+        if (ids[ord[i]] == ids[ord[i - 1]])
+            throw std::invalid_argument("RsFnt::decode: repeated fragment id");
+    return ord;
+}
+
+bool marked_at(const Properties& p, size_t loc)
+{
+    for (auto const& it : p.get_map())
+        if (it.first == loc && it.second == OOR_MARK)
+            return true;
+    return false;
+}
+
+}  // namespace
+
+void RsFnt::encode(vec::Vector& output, std::vector<Properties>& props, off_t offset,
+                   const vec::Vector& words)
+{
+    // src/fec_rs_fnt.h:178-201: fft->fft(output, words) -- the n-point NTT of
+    // the zero-padded data whatever the type -- then encode_post_process: an
+    // output i < n_outputs equal to 65536 is marked at `offset` and set to 0
+    if (words.size() < n_data || output.size() < n || props.size() < n_outputs)
+        throw std::invalid_argument("RsFnt::encode: vector sizes");
+    std::vector<uint16_t> in(n_data), out(n);
+    for (unsigned i = 0; i < n_data; i++) {
+        if (words[i] > 65535u)
+            throw std::invalid_argument("RsFnt::encode: data symbol >= 65536");
+        in[i] = static_cast<uint16_t>(words[i]);
+    }
+    std::vector<const uint8_t*> dp(n_data);
+    std::vector<uint8_t*> op(n);
+    for (unsigned i = 0; i < n_data; i++)
+        dp[i] = reinterpret_cast<const uint8_t*>(&in[i]);
+    for (unsigned i = 0; i < n; i++)
+        op[i] = reinterpret_cast<uint8_t*>(&out[i]);
+    std::vector<Properties> marks(n);
+    encode_columns(hplan(), dp.data(), op.data(), 1, marks, 0);
+    for (unsigned i = 0; i < n; i++)
+        output[i] = marks[i].get_map().empty() ? out[i] : 65536u;
+    for (unsigned i = 0; i < n_outputs; i++) {
+        if (output[i] == 65536u) {
+            props[i].add(static_cast<size_t>(offset), OOR_MARK);
+            output[i] = 0;
+        }
+    }
+    n_encode_ops++;
+}
+
+void RsFnt::encode(vec::Buffers& output, std::vector<Properties>& props, off_t offset,
+                   const vec::Buffers& words)
+{
+    // src/fec_rs_fnt.h:231-270: systematic -> the m parities (interpolation
+    // + NTT), otherwise the n outputs of the NTT; encode_post_process marks
+    // every 65536 of the first n_outputs rows at offset + j (the value stays)
+    const bool sys = type == FecType::SYSTEMATIC;
+    qi_plan* pl = sys ? plan_ : hplan();
+    const unsigned rows = sys ? n_parities : n;
+    const size_t size = words.get_size();
+    if (words.get_n() < static_cast<int>(n_data) || output.get_n() < static_cast<int>(rows) ||
+        output.get_size() < size || props.size() < n_outputs)
+        throw std::invalid_argument("RsFnt::encode: buffer sizes");
+    std::vector<std::vector<uint16_t>> in(n_data, std::vector<uint16_t>(size));
+    std::vector<std::vector<uint16_t>> out(rows, std::vector<uint16_t>(size));
+    for (unsigned i = 0; i < n_data; i++)
+        for (size_t j = 0; j < size; j++) {
+            const uint32_t v = words.get(static_cast<int>(i))[j];
+            if (v > 65535u)
+                throw std::invalid_argument("RsFnt::encode: data symbol >= 65536");
+            in[i][j] = static_cast<uint16_t>(v);
+        }
+    std::vector<const uint8_t*> dp(n_data);
+    std::vector<uint8_t*> op(rows);
+    for (unsigned i = 0; i < n_data; i++)
+        dp[i] = reinterpret_cast<const uint8_t*>(in[i].data());
+    for (unsigned i = 0; i < rows; i++)
+        op[i] = reinterpret_cast<uint8_t*>(out[i].data());
+    std::vector<Properties> marks(rows);
+    encode_columns(pl, dp.data(), op.data(), size, marks, 0);
+    for (unsigned i = 0; i < rows; i++) {
+        uint32_t* o = output.get(static_cast<int>(i));
+        for (size_t j = 0; j < size; j++)
+            o[j] = out[i][j];
+        for (auto const& it : marks[i].get_map()) {
+            o[it.first] = 65536u;
+            if (i < n_outputs)
+                props[i].add(static_cast<size_t>(offset) + it.first, OOR_MARK);
+        }
+    }
+    n_encode_ops++;
+}
+
+std::unique_ptr<DecodeContext> RsFnt::init_context_dec(const vec::Vector& fragments_ids,
+                                                       std::vector<Properties>& input_props,
+                                                       size_t size)
+{
+    // src/fec_base.h:758-793 (the props are read by each decode call)
+    (void)input_props;
+    if (fragments_ids.size() < n_data)
+        throw std::invalid_argument("RsFnt::init_context_dec: need n_data ids");
+    vec::Vector ids(fragments_ids.begin(), fragments_ids.begin() + n_data);
+    for (uint32_t id : ids)
+        if (id >= n)
+            throw std::invalid_argument("RsFnt::init_context_dec: fragment id >= n");
+    return std::make_unique<DecodeContext>(ids, size);
+}
+
+void RsFnt::decode(DecodeContext& context, vec::Vector& output,
+                   const std::vector<Properties>& props, off_t offset, vec::Vector& words)
+{
+    // decode_prepare (src/fec_base.h:799-820): a mark at `offset` on fragment
+    // ids[i] restores words[i] = 65536; decode_apply (:829-878) interpolates
+    // the n-point code: output = the k coefficients
+    const vec::Vector& ids = context.get_fragments_id();
+    if (words.size() < n_data || output.size() < n_data)
+        throw std::invalid_argument("RsFnt::decode: vector sizes");
+    std::vector<int> id(n_data);
+    std::vector<uint16_t> in(n_data), out(n_data);
+    std::vector<Properties> marks(n_data);
+    std::vector<const uint8_t*> rows(n_data);
+    std::vector<const Properties*> mp(n_data);
+    std::vector<uint8_t*> op(n_data);
+    // the device takes the received fragments in ascending id order (the
+    // interpolation does not depend on the order)
+    const std::vector<unsigned> ord = id_order(ids, n_data);
+    for (unsigned i = 0; i < n_data; i++) {
+        const unsigned r = ord[i];
+        if (ids[r] < props.size() && marked_at(props[ids[r]], static_cast<size_t>(offset)))
+            words[r] = 65536u;
+    }
+    for (unsigned i = 0; i < n_data; i++) {
+        const unsigned r = ord[i];
+        id[i] = static_cast<int>(ids[r]);
+        in[i] = static_cast<uint16_t>(words[r] & 0xffffu);
+        if (words[r] == 65536u)
+            marks[i].add(0, OOR_MARK);
+        rows[i] = reinterpret_cast<const uint8_t*>(&in[i]);
+        mp[i] = &marks[i];
+        op[i] = reinterpret_cast<uint8_t*>(&out[i]);
+    }
+    decode_columns(hplan(), id, rows, mp, op.data(), 1, 0);
+    for (unsigned i = 0; i < n_data; i++)
+        output[i] = out[i];
+    n_decode_ops++;
+}
+
+void RsFnt::decode(DecodeContext& context, vec::Buffers& output,
+                   const std::vector<Properties>& props, off_t offset, vec::Buffers& words)
+{
+    // decode_prepare (src/fec_base.h:1361-1404): the marks of the received
+    // coded fragments (props by parity index) inside [offset, offset + size)
+    // restore 65536; decode_apply (:1418-1448) + for systematic codes the
+    // evaluation at r^t (:1336-1355): output = the k data rows
+    const bool sys = type == FecType::SYSTEMATIC;
+    const vec::Vector& ids = context.get_fragments_id();
+    const size_t size = words.get_size();
+    if (words.get_n() < static_cast<int>(n_data) || output.get_n() < static_cast<int>(n_data) ||
+        output.get_size() < size)
+        throw std::invalid_argument("RsFnt::decode: buffer sizes");
+    std::vector<int> id(n_data);
+    std::vector<std::vector<uint16_t>> in(n_data, std::vector<uint16_t>(size)),
+        out(n_data, std::vector<uint16_t>(size));
+    std::vector<Properties> marks(n_data);
+    std::vector<const uint8_t*> rows(n_data);
+    std::vector<const Properties*> mp(n_data);
+    std::vector<uint8_t*> op(n_data);
+    const std::vector<unsigned> ord = id_order(ids, n_data);
+    for (unsigned i = 0; i < n_data; i++) {
+        const unsigned r = ord[i];
+        id[i] = static_cast<int>(ids[r]);
+        uint32_t* w = words.get(static_cast<int>(r));
+        if (!(sys && ids[r] < n_data)) {
+            const size_t pi = sys ? ids[r] - n_data : ids[r];
+            if (pi < props.size())
+                for (auto const& it : props[pi].get_map())
+                    if (it.second == OOR_MARK && it.first >= static_cast<size_t>(offset) &&
+                        it.first < static_cast<size_t>(offset) + size)
+                        w[it.first - static_cast<size_t>(offset)] = 65536u;
+        }
+        for (size_t j = 0; j < size; j++) {
+            in[i][j] = static_cast<uint16_t>(w[j] & 0xffffu);
+            if (w[j] == 65536u)
+                marks[i].add(j, OOR_MARK);
+        }
+        rows[i] = reinterpret_cast<const uint8_t*>(in[i].data());
+        mp[i] = &marks[i];
+        op[i] = reinterpret_cast<uint8_t*>(out[i].data());
+    }
+    decode_columns(plan_, id, rows, mp, op.data(), size, 0);
+    for (unsigned i = 0; i < n_data; i++) {
+        uint32_t* o = output.get(static_cast<int>(i));
+        for (size_t j = 0; j < size; j++)
+            o[j] = out[i][j];
+    }
+    n_decode_ops++;
 }
 
 // ----------------------------------------------------------------- RS-NF4
