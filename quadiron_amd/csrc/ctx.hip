@@ -116,7 +116,7 @@ __device__ __forceinline__ uint32_t grp_add(uint32_t v, int lpr)
     return v;
 }
 __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLayout& L,
-                             int t, int32_t* block, int sub, int lpr)
+                             int t, int32_t* block, int sub, int lpr, bool dot2)
 {
     // the lane's entries i = sub + m lpr (m < 16: k <= 256 at lpr = 16) in
     // registers: every row load is issued up front (rows in global memory
@@ -169,7 +169,7 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
             row[i] = v[m];
             plain[static_cast<size_t>(t) * kin + i] = static_cast<int32_t>(v[m]);
             sum += v[m];
-            if (!(sub & 1)) {
+            if (dot2 && !(sub & 1)) {
                 const int32_t lo = balanced(v[m]);
                 const int32_t hi = i + 1 < kin ? balanced(odd) : 0;
                 packed[i >> 1] = static_cast<int32_t>((static_cast<uint32_t>(lo) & 0xffffu) |
@@ -178,7 +178,7 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
         }
     }
     // pairs past kin up to KP stay zero (the dot2 kernel's padding)
-    for (int j = (kin + 1) / 2 + sub; j < KP; j += lpr)
+    for (int j = (kin + 1) / 2 + sub; dot2 && j < KP; j += lpr)
         packed[j] = 0;
     sum = grp_add(sum, lpr);
     if (sub == 0) {
@@ -205,7 +205,7 @@ template <int NT, bool BIG>
 __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
     int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
-    int by_pos, long long words, uint32_t* err)
+    int by_pos, long long words, int dot2, uint32_t* err)
 {
     __shared__ uint32_t xs[kMatMaxKin];
     __shared__ uint32_t A[kMatMaxKin + 1];
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         const int q4 = (k + 3) / 4;
         const int lpr = q4 <= 4 ? 4 : q4 <= 8 ? 8 : q4 <= 16 ? 16 : 32;
         for (int t = tid / lpr; t < L.R; t += NT / lpr)
-            pack_row_grp(Mt + t * kp, cinv, L, t, mat, tid & (lpr - 1), lpr);
+            pack_row_grp(Mt + t * kp, cinv, L, t, mat, tid & (lpr - 1), lpr, dot2 != 0);
     }
     if (L.KS()) {
         // the matrix-core operand tiles, from the row-scaled entries in LDS
@@ -496,7 +496,7 @@ template <int NT>
 __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
     int k, RPow2 rp, int lgn, int mode, MatLayout L,
     const uint16_t* __restrict__ ids, int32_t* __restrict__ ctx, long long ctx_stride,
-    Oor in_oor, int slot_base, int by_pos, long long words, uint32_t* err)
+    Oor in_oor, int slot_base, int by_pos, long long words, int dot2, uint32_t* err)
 {
     __shared__ uint32_t xs[128];
     __shared__ int32_t A[129];        // balanced coefficients of A(x)
@@ -760,10 +760,16 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
             }
         }
     }
-    // the canonical `plain` rows and the dot2 kernel's packed pairs: items
-    // entries-fastest, so a wave's stores are contiguous runs (rows-fastest
-    // 16-byte pieces scattered over the rows had made the round-1 context
-    // store-bound)
+    // the canonical `plain` rows and the dot2 kernel's packed pairs, only
+    // for widths with a column tail (dot2): the matrix-core kernels read the
+    // tiles alone (their OOR restore and the redo kernel take single
+    // coefficients back from the tiles), and fill_dot2_sections writes these
+    // two from the tiles if a whole-tile decode ever needs the dot2 kernel
+    // (rows the matrix cores cannot address).  Items entries-fastest, so a
+    // wave's stores are contiguous runs (rows-fastest 16-byte pieces
+    // scattered over the rows had made the round-1 context store-bound)
+    if (!dot2)
+        return;
     int32_t* plain = mat + L.plain();
     const int ng = (k + 3) / 4;
     for (int it = tid; it < L.R * ng; it += NT) {
@@ -792,10 +798,45 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         mat[static_cast<size_t>(it / npz) * L.KP + pz + it % npz] = 0;
 }
 
+// The dot2 sections (packed pairs, canonical `plain` rows) of contexts built
+// without them (whole-tile widths, dot2 = 0), from their operand tiles: for
+// a decode whose rows the matrix cores cannot address (launch_matrix then
+// runs the dot2 kernel over every column).  Decode contexts hold rows the
+// dot2 kernel can take (coef_ok), so the balanced entries fit its pairs.
+__global__ __launch_bounds__(256) void fill_dot2_kernel(MatLayout L, int32_t* ctx, long long cs)
+{
+    int32_t* mat = ctx + blockIdx.x * cs;
+    const int32_t* mf = mat + L.mf();
+    int32_t* plain = mat + L.plain();
+    for (int it = threadIdx.x; it < L.R * L.KP; it += 256) {
+        const int t = it / L.KP, j = it - t * L.KP, i = 2 * j;
+        int32_t v[2] = {0, 0};
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            if (i + h < L.kin) {
+                const uint32_t e = mf_entry(L, mf, t, i + h);
+                plain[static_cast<size_t>(t) * L.kin + i + h] = static_cast<int32_t>(e);
+                v[h] = balanced(e);
+            }
+        }
+        mat[static_cast<size_t>(t) * L.KP + j] = static_cast<int32_t>(
+            (static_cast<uint32_t>(v[0]) & 0xffffu) | (static_cast<uint32_t>(v[1]) << 16));
+    }
+}
+
+int fill_dot2_sections(const MatLayout& L, int32_t* d_ctx, long long ctx_stride, int S,
+                       hipStream_t st)
+{
+    if (S <= 0)
+        return 0;
+    hipLaunchKernelGGL(fill_dot2_kernel, dim3(S), dim3(256), 0, st, L, d_ctx, ctx_stride);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
                       const uint16_t* d_ids, int S, int32_t* d_ctx,
                       long long ctx_stride, const Oor* in_oor, int slot_base,
-                      int by_pos, long long words, uint32_t* err, hipStream_t st)
+                      int by_pos, long long words, int dot2, uint32_t* err, hipStream_t st)
 {
     if (k > kMatMaxKin || S <= 0)
         return -3;
@@ -806,7 +847,7 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
         // (k256 decode 0.81 -> 0.77 ms, k200 2.09 -> 2.05 ms)
         hipLaunchKernelGGL((decode_ctx_kernel<1024, true>), dim3(S), dim3(1024), 0, st, k, r,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                           slot_base, by_pos, words, err);
+                           slot_base, by_pos, words, dot2, err);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     RPow2 rp{};
@@ -828,11 +869,11 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
     if (k > 32)
         hipLaunchKernelGGL((decode_ctx_lds_kernel<256>), dim3(S), dim3(256), lds, st, k, rp, lgn,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                           slot_base, by_pos, words, err);
+                           slot_base, by_pos, words, dot2, err);
     else
         hipLaunchKernelGGL((decode_ctx_lds_kernel<128>), dim3(S), dim3(128), lds, st, k, rp, lgn,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                           slot_base, by_pos, words, err);
+                           slot_base, by_pos, words, dot2, err);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -578,8 +578,9 @@ __device__ __forceinline__ void push_slow_tile(const SlowList& sl, int s, long l
 // kRedoCols columns: the chunk's received symbols (u16) and a bitmap of
 // their marks staged in LDS (every mark of every received row, from the
 // buckets), then lane c of wave wv recomputes column c for the output rows
-// wv, wv + 4, ... (the coefficient plain[t][j] is wave-uniform: scalar
-// loads) -- only in columns that hold a mark.  Work per chunk is
+// wv, wv + 4, ... (the coefficient, read back from the operand tiles by
+// mf_entry, is wave-uniform: scalar loads) -- only in columns that hold a
+// mark.  Work per chunk is
 // R * kin * 64 multiply-adds whatever the mark density (walking the marks
 // per (mark, row, input) was quadratic in the density).  The stripe's list
 // is emptied afterwards (a context can serve several decodes).
@@ -604,7 +605,7 @@ __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_st
         const int32_t* M = a.mat + s * a.ms;
         const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
         const int32_t* rscale = M + L.rscale();
-        const int32_t* plain = M + L.plain();
+        const int32_t* mf = M + L.mf();
         auto id_of = [&](int i) { return src.by_pos ? i : (sid ? sid[i] : i); };
         for (uint32_t e = 0; e < n; e++) {
             const uint32_t code = l[1 + e];
@@ -650,8 +651,7 @@ __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_st
                                 (mk[j * (kRedoCols / 32) + c / 32] >> (c % 32)) & 1u
                                     ? 65536u
                                     : xs[j * kRedoCols + c];
-                            acc += static_cast<uint64_t>(
-                                       static_cast<uint32_t>(plain[t * kin + j])) * x;
+                            acc += static_cast<uint64_t>(mf_entry(L, mf, t, j)) * x;
                         }
                         uint32_t y = static_cast<uint32_t>(acc % 65537u);
                         const int32_t rs = rscale[t];
@@ -1151,7 +1151,6 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     const int32_t* mf = M + L.mf();
     const int32_t* kmf = M + L.kmf();
     const int32_t* rscale = M + L.rscale_mf();
-    const int32_t* plain = M + L.plain();
     const int32_t* __restrict__ rowmap = a.rowmap;
     auto load_ops = [&](int rb, qi_v2i (&b)[KS][3], int32_t& kt, int32_t& rs, int32_t (&pr)[3]) {
 #pragma unroll
@@ -1387,7 +1386,16 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
                 const int pos = __builtin_amdgcn_readfirstlane(s_i[e]);
                 const long long wc = wcu;
                 const long long d = wc - cb;
-                const int32_t corr = plain[tcl * kin + pos];
+                // from the operand tile in registers (bop[ks][2] = [b | a])
+                const int32_t corr = coef_from_tiles<KS>(
+                    [&](int idx) {
+                        int32_t r = 0;
+#pragma unroll
+                        for (int q = 0; q < 2 * KS; q++)
+                            r = idx == q ? bop[q >> 1][2][q & 1] : r;
+                        return r;
+                    },
+                    pos, l);
 #pragma unroll
                 for (int c = 0; c < 16; c++) {
                     const int32_t yc = fold(fold(y[c] - corr));
@@ -1566,14 +1574,28 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
 // matrix_mfma_kernel's (byte split, 2^16 = -1, D2 folded first at KS = 16).
 // ---------------------------------------------------------------------------
 // Coefficient M[t][pos] of this lane's output row t (lane (g, t & 15) of a
-// 16-row block) from the block's [b | a] operand tile, held in registers as
-// KS / 2 v4i (x64 pairs; lane 16 g + t, dword 2 ks + dw: bytes K = 32 ks +
-// 8 g + 4 dw + 0..3, b at K = pos and a at K = 16 KS + pos): the row-scaled
-// entry as 256 a + b (balanced), the value the `plain` section holds.  pos is
-// wave-uniform; the two dwords come from the lane holding them by
-// ds_bpermute.
+// 16-row block) from the block's [b | a] operand tile held in registers:
+// pick(2 ks + dw) returns this lane's dword dw of K-step ks (lane 16 g + t:
+// bytes K = 32 ks + 8 g + 4 dw + 0..3; b at K = pos, a at K = 16 KS + pos,
+// pack_mf_dword's layout).  Returns the row-scaled entry as 256 a + b
+// (balanced), the value of mf_entry / the `plain` section; pos is
+// wave-uniform, and each byte comes from the lane holding it by ds_bpermute
+// -- no memory load (waiting for one drains the stores and prefetches).
+template <int KS, class Pick>
+__device__ __forceinline__ int32_t coef_from_tiles(const Pick& pick, int pos, int lane)
+{
+    constexpr int KH = 16 * KS;
+    auto byte_at = [&](int K) {
+        const int ks = K >> 5, g = (K & 31) >> 3, dw = (K >> 2) & 1, sh = 8 * (K & 3);
+        const int32_t x = __shfl(pick(2 * ks + dw), 16 * g + (lane & 15));
+        return (x << (24 - sh)) >> 24;
+    };
+    return 256 * byte_at(KH + pos) + byte_at(pos);
+}
+
+// uniform-index selection among a wave's operand dwords (a v_cndmask chain)
 template <int NP>
-__device__ __forceinline__ int32_t pick_dw(const qi_v4i (&v)[NP], int idx)
+__device__ __forceinline__ int32_t pick_v4(const qi_v4i (&v)[NP], int idx)
 {
     int32_t r = 0;
 #pragma unroll
@@ -1582,19 +1604,6 @@ __device__ __forceinline__ int32_t pick_dw(const qi_v4i (&v)[NP], int idx)
         for (int e = 0; e < 4; e++)
             r = idx == 4 * i + e ? v[i][e] : r;
     return r;
-}
-
-template <int NP>
-__device__ __forceinline__ int32_t coef_from_tiles(const qi_v4i (&b2)[NP], int pos, int lane)
-{
-    constexpr int KS = 2 * NP;
-    const int ks = pos >> 5, g = (pos & 31) >> 3, dw = (pos >> 2) & 1, sh = 8 * (pos & 3);
-    const int32_t vb = pick_dw(b2, 2 * ks + dw);
-    const int32_t va = pick_dw(b2, 2 * (ks + KS / 2) + dw);
-    const int src = 16 * g + (lane & 15);
-    const int32_t xb = __shfl(vb, src), xa = __shfl(va, src);
-    const int32_t b = (xb << (24 - sh)) >> 24, a = (xa << (24 - sh)) >> 24;
-    return 256 * a + b;
 }
 
 template <int KS, int WR>
@@ -1663,7 +1672,6 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     const int32_t* mf = M + L.mf();
     const int32_t* kmf = M + L.kmf();
     const int32_t* rscale = M + L.rscale_mf();
-    const int32_t* plain = M + L.plain();
     const int32_t* __restrict__ rowmap = a.rowmap;
     const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
 
@@ -1874,7 +1882,8 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             const long long d = static_cast<long long>(wcu) - cb;
             // the coefficient from the wave's own operand tiles (no memory
             // load: waiting for one drained the stores and the prefetch)
-            const int32_t corr = coef_from_tiles(b2[j], pos, l);
+            const int32_t corr = coef_from_tiles<KS>(
+                [&](int idx) { return pick_v4(b2[j], idx); }, pos, l);
 #pragma unroll
             for (int c = 0; c < 16; c++) {
                 const int32_t yc = fold(fold(y[c] - corr));

@@ -45,6 +45,18 @@ long long mat_ctx_words(const qi_plan* p, long long words)
            route_tiles(words) * kRouteStride + slow_words(words);
 }
 
+// A context built for a whole-tile width carries only the matrix-core
+// form; rows the matrix cores cannot address send every column to the dot2
+// kernel, whose sections are filled from the tiles first (idempotent)
+int complete_dot2(const qi_plan* p, const void* d_ctx, long long cs, long long words, int S,
+                  hipStream_t s)
+{
+    if (words % kRouteTile != 0)
+        return 0;  // built with them
+    return fill_dot2_sections(ctx_layout(p), static_cast<int32_t*>(const_cast<void*>(d_ctx)),
+                              cs, S, s);
+}
+
 }  // namespace
 
 namespace qi {
@@ -89,9 +101,13 @@ int build_ctx(qi_plan* p, const uint16_t* d_ids, int n_stripes, const Oor* in,
         if (rc)
             return rc;
     }
+    // the dot2 sections only for widths with a column tail (below 256 < k:
+    // no dot2 kernel at all); a whole-tile decode that needs them after all
+    // fills them from the tiles (qi_gpu_decode)
+    const int dot2 = !p->mbig && words % kRouteTile != 0;
     return launch_decode_ctx(p->k, p->n, p->r, p->sys ? 1 : 0, L, d_ids, n_stripes,
                              static_cast<int32_t*>(d_ctx), cs, in, slot_base, by_pos,
-                             words, p->d_err, s);
+                             words, dot2, p->d_err, s);
 }
 
 }  // namespace qi
@@ -190,10 +206,14 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
     if (!use_matrix(p, words))
         return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, p->sys ? p->k : 0, out,
                           words, n_stripes, st(stream));
-    if (p->mbig && !matrix_cores_take(src, out, L.R, words))
-        return ntt_decode(p, ctx + mat_ctx_words(p, words), cs, src,
-                          d_counts ? &in : nullptr, p->sys ? p->k : 0, out, words, n_stripes,
-                          st(stream));
+    if (!matrix_cores_take(src, out, L.R, words)) {
+        if (p->mbig)
+            return ntt_decode(p, ctx + mat_ctx_words(p, words), cs, src,
+                              d_counts ? &in : nullptr, p->sys ? p->k : 0, out, words,
+                              n_stripes, st(stream));
+        if (int rc = complete_dot2(p, d_ctx, cs, words, n_stripes, st(stream)))
+            return rc;
+    }
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, p->sys ? p->k : 0,
                          nullptr, p->d_rowid,
@@ -235,9 +255,14 @@ int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
     if (!use_matrix(p, words))
         return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, 0, out, words,
                           n_stripes, st(stream));
-    if (p->mbig && !matrix_cores_take(src, out, L.R, words))
-        return ntt_decode(p, ctx + mat_ctx_words(p, words), cs, src, d_counts ? &in : nullptr,
-                          0, out, words, n_stripes, st(stream));
+    if (!matrix_cores_take(src, out, L.R, words)) {
+        if (p->mbig)
+            return ntt_decode(p, ctx + mat_ctx_words(p, words), cs, src,
+                              d_counts ? &in : nullptr, 0, out, words, n_stripes,
+                              st(stream));
+        if (int rc = complete_dot2(p, d_ctx, cs, words, n_stripes, st(stream)))
+            return rc;
+    }
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, 0, nullptr, p->d_rowid,
                          reinterpret_cast<const uint32_t*>(ctx + L.words() + 2 * L.KP),

@@ -116,11 +116,17 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long mat_stride,
 //   (slow_words(words) u32, count cleared)
 //   (slot = by_pos ? position : id - slot_base); in_oor may be null.
 //   n: the code length (ids < n), r its root of unity
+//   dot2: also write the dot2 kernel's sections (packed pairs, `plain`
+//   rows); without them only the matrix cores can apply the context
 int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
                       const uint16_t* d_ids, int n_stripes, int32_t* d_ctx,
                       long long ctx_stride, const Oor* in_oor, int slot_base,
-                      int by_pos, long long words, uint32_t* d_err,
+                      int by_pos, long long words, int dot2, uint32_t* d_err,
                       hipStream_t stream);
+// the dot2 sections of n_stripes contexts built with dot2 = 0, from their
+// operand tiles (before a decode that runs the dot2 kernel over them)
+int fill_dot2_sections(const MatLayout& L, int32_t* d_ctx, long long ctx_stride, int n_stripes,
+                       hipStream_t stream);
 
 // matrix kernel instantiation choice
 int matrix_kp(int kin);

@@ -476,16 +476,23 @@ def test_decode_row_scales_many_stripes(k, m, S, P):
     _batch_roundtrip(k, m, 0, S, P, seed=3 * k + S, n_craft=0, check_oracle=False)
 
 
-@pytest.mark.parametrize("sys_", [0, 1])
-def test_big_matrix_path_unaligned_rows(sys_):
-    """256 < k <= 384 at a whole-tile width (1024 columns) but with rows the
-    matrix cores cannot address (base offset by one u16, odd row strides):
-    the encode runs the NTT engine and the decode uses the NTT context that
-    follows the matrix one (these calls used to fail with -3)."""
+@pytest.mark.parametrize("k,m,sys_", [
+    (300, 100, 0), (300, 100, 1),   # 256 < k <= 384: the NTT engine takes them
+    (16, 48, 0), (64, 960, 0), (200, 56, 1),  # the dot2 kernel, its context
+                                              # sections filled from the tiles
+])
+def test_unaligned_rows_whole_tiles(k, m, sys_):
+    """A whole-tile width (1024 columns) with rows the matrix cores cannot
+    address (base offset by one u16, odd row strides).  256 < k <= 384: the
+    encode runs the NTT engine and the decode the NTT context kept behind the
+    matrix one (these calls used to fail with -3).  k <= 256: the
+    context was built with the matrix-core form only (whole tiles), and the
+    decode fills the dot2 kernel's sections from the operand tiles first.
+    Then the same contexts decode aligned copies on the matrix cores."""
     torch = _torch()
     import quadiron_amd as qa
-    k, m, S, P = 300, 100, 2, 1024
-    rng = np.random.default_rng(300 + sys_)
+    S, P = 2, 1024
+    rng = np.random.default_rng(k + 300 + sys_)
     plan = qa.Plan(k, m, sys_)
     no = plan.n_outputs
     data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
