@@ -467,6 +467,10 @@ struct NttLdsArgs {
     uint32_t* err;
     int wide;  // 16-byte row pieces: every row base and stride 8-word
                // aligned and words % 8 == 0 (lds_launch checks)
+    // erasure decode (ntt_eras_kernel): e erased positions, their list and
+    // the e x e solve in the context, n^-1 (balanced)
+    int eras_e, eras_eid, eras_b;
+    int32_t inv_n;
 };
 
 // One pass over the image: tasks (group start b, offset j < s) of the R
@@ -859,6 +863,338 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Erasure decode (plans with few erasures: e = n - k <= kErasMax, n <= 2048,
+// eras_plan).  The codeword of both types is c_j = P(r^j), deg P < k, over
+// all n positions (those >= k + m are never sent); a stripe receives k of
+// them and misses the e positions E.  The unnormalised INTT_n of the
+// zero-filled codeword, y', holds e "syndromes" in its top outputs
+// (y'_t = -sum_{j in E} c_j r^-jt for t >= k, where the true coefficients
+// vanish), and with x_j = r^-E_j the erased symbols solve a transposed
+// Vandermonde system:
+//     c_E = B y'_[k, n),   B[j][u] = -r^(E_j k) coef_u(L_j),
+//     L_j = prod_{l != j} (X - x_l) / (x_j - x_l)          (per pattern)
+// Then the systematic outputs ARE codeword symbols (received rows copied,
+// erased ones from c_E), and the non-systematic coefficients are one more
+// INTT_n of the completed codeword times n^-1.  So a decode is 1 or 2
+// n-point transforms + e^2 multiply-adds per column instead of decode_apply's
+// INTT_n + NTT_2k + INTT_2k (+ NTT_n) (src/fec_base.h:1418-1448), the same
+// outputs (the interpolation is unique), on an n-row image; the systematic
+// encode is the same solve with E = [k, n) (the plan's constant context).
+// The math is emulated in tests/test_ntt_plan.py::test_erasure_decode_math.
+// ---------------------------------------------------------------------------
+constexpr int kErasMax = 64;
+
+struct ErasCtxLayout {
+    int k, n, e;
+    __host__ __device__ long long ids_off() const { return 0; }
+    __host__ __device__ long long pos_off() const { return k; }  // id -> i, or -1 - j (erased)
+    __host__ __device__ long long eid_off() const { return static_cast<long long>(k) + n; }
+    __host__ __device__ long long b_off() const { return eid_off() + e; }
+    __host__ __device__ long long words() const { return b_off() + static_cast<long long>(e) * e; }
+};
+
+struct ErasCtxArgs {
+    ErasCtxLayout L;
+    uint32_t r, rinv;     // n-th root of unity and its inverse
+    const uint16_t* ids;  // S x k received ids, ascending (nullptr: 0 .. k-1)
+    int32_t* ctx;
+    long long cs;
+};
+
+// One wave per stripe: the received bitmap, the erased list E (ascending),
+// x_j = r^-E_j, A(X) = prod (X - x_j) with lane d on coefficient d (the
+// monic top coefficient stays implicit), then lane j's synthetic division
+// Q_j = A / (X - x_j) into LDS and A'(x_j) = Q_j(x_j) beside it, and row j
+// of B.  O(e^2) per stripe, e <= 64.
+__global__ __launch_bounds__(64) void eras_ctx_kernel(ErasCtxArgs a)
+{
+    __shared__ uint32_t bm[kLdsMaxN / 32];
+    __shared__ int32_t eid[kErasMax];
+    __shared__ uint32_t W[kErasMax * kErasMax];
+    const int s = blockIdx.x, lane = threadIdx.x;
+    const int k = a.L.k, n = a.L.n, e = a.L.e, nw = n >> 5;
+    int32_t* ctx = a.ctx + s * a.cs;
+    int32_t* ids = ctx + a.L.ids_off();
+    int32_t* pos = ctx + a.L.pos_off();
+    const uint16_t* sid = a.ids ? a.ids + static_cast<long long>(s) * k : nullptr;
+    for (int w = lane; w < nw; w += 64)
+        bm[w] = 0;
+    __syncthreads();
+    for (int i = lane; i < k; i += 64) {
+        const int id = sid ? sid[i] : i;
+        ids[i] = id;
+        pos[id] = i;
+        atomicOr(&bm[id >> 5], 1u << (id & 31));
+    }
+    __syncthreads();
+    // erased positions in ascending order: lane w takes bitmap word w (at
+    // most 64 words), its slot offset from an exclusive scan of the counts
+    uint32_t miss = lane < nw ? ~bm[lane] : 0u;
+    int cnt = __popc(miss), off = cnt;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(off, d);
+        if (lane >= d)
+            off += v;
+    }
+    off -= cnt;
+    while (miss) {
+        const int b = __ffs(miss) - 1;
+        miss &= miss - 1;
+        const int t = lane * 32 + b;
+        eid[off] = t;
+        ctx[a.L.eid_off() + off] = t;
+        pos[t] = -1 - off;
+        off++;
+    }
+    __syncthreads();
+    const uint32_t xj = lane < e ? powm_(a.rinv, static_cast<uint32_t>(eid[lane])) : 0u;
+    uint32_t ad = lane == 0 ? 1u : 0u;  // A, coefficient `lane`
+    for (int j = 0; j < e; j++) {
+        const uint32_t x = __builtin_amdgcn_readlane(xj, j);
+        uint32_t prev = __shfl_up(ad, 1);
+        prev = lane == 0 ? 0u : prev;
+        ad = subm_(prev, mulm_(x, ad));
+    }
+    uint32_t q = 1, h = 1;  // q_{e-1} = 1 (A monic); Horner of Q_j at x_j
+    if (lane < e)
+        W[lane * kErasMax + e - 1] = 1;
+    for (int t = e - 1; t >= 1; t--) {
+        const uint32_t at = __builtin_amdgcn_readlane(ad, t);
+        q = addm_(at, mulm_(xj, q));
+        h = addm_(mulm_(h, xj), q);
+        if (lane < e)
+            W[lane * kErasMax + t - 1] = q;
+    }
+    if (lane < e) {
+        // f_j = -r^(E_j k) / A'(x_j)
+        const uint32_t rk = powm_(a.r, static_cast<uint32_t>(
+                                           (static_cast<long long>(eid[lane]) * k) % n));
+        const uint32_t f = subm_(0u, mulm_(rk, powm_(h, 65535u)));
+        int32_t* B = ctx + a.L.b_off() + static_cast<long long>(lane) * e;
+        for (int u = 0; u < e; u++)
+            B[u] = balanced(mulm_(f, W[lane * kErasMax + u]));
+    }
+}
+
+// The erasure decode of a tile of T columns of one stripe (and the
+// systematic encode, E = [k, n)), in LDS: image n x T, then the tables
+// (unless TWG), ids, the position map, E, B and c_E (e x T).
+template <bool TWG>
+__global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
+{
+    extern __shared__ int32_t qi_ntt_lds[];
+    const int n = a.n, lgT = a.lgT, T = 1 << lgT, k = a.k, e = a.eras_e;
+    int32_t* buf = qi_ntt_lds;
+    int32_t* tw_l = buf + (n << lgT);
+    const int32_t* tw = TWG ? a.tw : tw_l;
+    int32_t* s_id = TWG ? tw_l : tw_l + a.tw_words;
+    int32_t* s_pos = s_id + k;
+    int32_t* s_eid = s_pos + n;
+    int32_t* s_B = s_eid + e;
+    int32_t* s_cE = s_B + e * e;
+    int b = blockIdx.x;  // XCD-contiguous tiles, as ntt_lds_kernel
+    if ((gridDim.x & 7) == 0)
+        b = (b & 7) * static_cast<int>(gridDim.x >> 3) + (b >> 3);
+    const int s = b / a.tiles;
+    const long long c0 = static_cast<long long>(b - s * a.tiles) << lgT;
+    const int tid = threadIdx.x, col = tid & (T - 1), g = tid >> lgT, G = kLdsThreads >> lgT;
+    const long long cg = c0 + col;
+    const bool valid = cg < a.words;
+    const int32_t* ctx = a.ctx + s * a.cs;
+    if (!TWG)
+        for (int i = tid; i < a.tw_words; i += kLdsThreads)
+            tw_l[i] = a.tw[i];
+    for (int i = tid; i < k; i += kLdsThreads)
+        s_id[i] = ctx[a.ids_off + i];
+    for (int t = tid; t < n; t += kLdsThreads)
+        s_pos[t] = ctx[a.pos_off + t];
+    for (int j = tid; j < e; j += kLdsThreads)
+        s_eid[j] = ctx[a.eras_eid + j];
+    for (int i = tid; i < e * e; i += kLdsThreads)
+        s_B[i] = ctx[a.eras_b + i];
+    __syncthreads();
+    const RowSrc& src = a.src;
+    auto row_ptr = [&](int id) {
+        return id < src.split ? src.base0 + s * src.ss0 + id * src.rs0
+                              : src.base1 + s * src.ss1 + (id - src.split) * src.rs1;
+    };
+    const int lgL = lgT - 3, rl = tid >> lgL, cj = tid & ((1 << lgL) - 1);
+    const int RPP = kLdsThreads >> lgL;
+    const long long cw = c0 + 8 * cj;
+    const bool wvalid = cw < a.words;
+    // the received rows at pos(id) (+ c_E at pos(E_j) when `fill`), the
+    // marked symbols as 65536 = -1 (decode_prepare, src/fec_base.h:1361-1404)
+    auto load = [&](bool fill) {
+        if (a.wide) {
+            for (int i0 = rl; i0 < k; i0 += RPP * kLdsBatch) {
+                uint4 x[kLdsBatch];
+#pragma unroll
+                for (int u = 0; u < kLdsBatch; u++) {
+                    const int i = i0 + u * RPP;
+                    x[u] = (i < k && wvalid) ? *reinterpret_cast<const uint4*>(
+                                                   row_ptr(src.by_pos ? i : s_id[i]) + cw)
+                                             : uint4{0, 0, 0, 0};
+                }
+#pragma unroll
+                for (int u = 0; u < kLdsBatch; u++) {
+                    const int i = i0 + u * RPP;
+                    if (i < k) {
+                        const uint32_t xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+                        int4* d = reinterpret_cast<int4*>(
+                            buf + (xf_pos(a.pni, s_id[i]) << lgT) + 8 * cj);
+                        d[0] = int4{static_cast<int32_t>(xs[0] & 0xffffu),
+                                    static_cast<int32_t>(xs[0] >> 16),
+                                    static_cast<int32_t>(xs[1] & 0xffffu),
+                                    static_cast<int32_t>(xs[1] >> 16)};
+                        d[1] = int4{static_cast<int32_t>(xs[2] & 0xffffu),
+                                    static_cast<int32_t>(xs[2] >> 16),
+                                    static_cast<int32_t>(xs[3] & 0xffffu),
+                                    static_cast<int32_t>(xs[3] >> 16)};
+                    }
+                }
+            }
+        } else {
+            for (int i0 = g; i0 < k; i0 += G * kLdsBatch) {
+                int32_t x[kLdsBatch];
+#pragma unroll
+                for (int u = 0; u < kLdsBatch; u++) {
+                    const int i = i0 + u * G;
+                    x[u] = (i < k && valid) ? row_ptr(src.by_pos ? i : s_id[i])[cg] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < kLdsBatch; u++) {
+                    const int i = i0 + u * G;
+                    if (i < k)
+                        buf[(xf_pos(a.pni, s_id[i]) << lgT) + col] = x[u];
+                }
+            }
+        }
+        for (int it = tid; it < (e << lgT); it += kLdsThreads) {
+            const int j = it >> lgT, c = it & (T - 1);
+            buf[(xf_pos(a.pni, s_eid[j]) << lgT) + c] = fill ? s_cE[it] : 0;
+        }
+        __syncthreads();
+        if (a.in_oor.counts) {
+            for (int i = tid; i < k; i += kLdsThreads) {
+                const int id = s_id[i];
+                const int slot = src.by_pos ? i : id - a.slot_base;
+                if (slot < 0)
+                    continue;  // systematic data row: no marks
+                const long long bk = static_cast<long long>(s) * a.in_oor.slots + slot;
+                uint32_t cnt = a.in_oor.counts[bk];
+                if (cnt > static_cast<uint32_t>(a.in_oor.cap)) {
+                    atomicOr(a.err, kErrOorTruncated);
+                    cnt = static_cast<uint32_t>(a.in_oor.cap);
+                }
+                const int p = xf_pos(a.pni, id);
+                for (uint32_t f = 0; f < cnt; f++) {
+                    const long long c = static_cast<long long>(
+                                            a.in_oor.entries[bk * a.in_oor.cap + f]) - c0;
+                    if (c >= 0 && c < T)
+                        buf[(p << lgT) + static_cast<int>(c)] = -1;
+                }
+            }
+            __syncthreads();
+        }
+    };
+    load(false);
+    lds_transform<false, true>(buf, tw, a.pni, lgT, col, g, G);
+    // c_E = B y'_[k, n): e lazy products per (erasure, column) item
+    for (int it = tid; it < (e << lgT); it += kLdsThreads) {
+        const int j = it >> lgT, c = it & (T - 1);
+        const int32_t* Bj = s_B + j * e;
+        int32_t acc = 0;  // |acc| <= 64 * 65536
+        for (int u = 0; u < e; u++)
+            acc += mul_rt(buf[((k + u) << lgT) + c], Bj[u]);
+        s_cE[it] = fold(fold(acc));  // [-1, 65536]
+    }
+    __syncthreads();
+    auto store8 = [&](uint16_t* o, const uint32_t (&cv)[8]) {
+        uint4 v;
+        v.x = (cv[0] & 0xffffu) | (cv[1] << 16);
+        v.y = (cv[2] & 0xffffu) | (cv[3] << 16);
+        v.z = (cv[4] & 0xffffu) | (cv[5] << 16);
+        v.w = (cv[6] & 0xffffu) | (cv[7] << 16);
+        *reinterpret_cast<uint4*>(o) = v;
+    };
+    auto record = [&](int r, long long c) {
+        const long long bk = static_cast<long long>(s) * a.out_oor.slots + r;
+        const uint32_t en = atomicAdd(&a.out_oor.counts[bk], 1u);
+        if (en < static_cast<uint32_t>(a.out_oor.cap))
+            a.out_oor.entries[bk * a.out_oor.cap + en] = static_cast<uint32_t>(c);
+    };
+    if (a.mode == kLdsDec) {
+        // the completed codeword -> INTT_n -> the k coefficients (x n^-1)
+        load(true);
+        lds_transform<false, true>(buf, tw, a.pni, lgT, col, g, G);
+        if (a.wide) {
+            if (!wvalid)
+                return;
+            for (int r = rl; r < a.out_rows; r += RPP) {
+                const int4* sp = reinterpret_cast<const int4*>(buf + (r << lgT) + 8 * cj);
+                const int4 lo = sp[0], hi = sp[1];
+                const int32_t v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+                uint32_t cv[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    cv[q] = canon_vr(fold(mul_rt(v[q], a.inv_n)));
+                store8(a.out + s * a.oss + r * a.ors + cw, cv);
+            }
+            return;
+        }
+        if (!valid)
+            return;
+        for (int r = g; r < a.out_rows; r += G)
+            a.out[s * a.oss + r * a.ors + cg] = static_cast<uint16_t>(
+                canon_vr(fold(mul_rt(buf[(r << lgT) + col], a.inv_n))));
+        return;
+    }
+    // systematic (decode: the data rows t < k; encode: the parities t >= k):
+    // codeword symbols, received ones copied, erased ones from c_E
+    if (a.wide) {
+        if (!wvalid)
+            return;
+        for (int r = rl; r < a.out_rows; r += RPP) {
+            const int t = a.out_first + r, pm = s_pos[t];
+            uint16_t* o = a.out + s * a.oss + r * a.ors + cw;
+            if (pm >= 0) {
+                *reinterpret_cast<uint4*>(o) =
+                    *reinterpret_cast<const uint4*>(row_ptr(src.by_pos ? pm : t) + cw);
+                continue;
+            }
+            const int32_t* ce = s_cE + ((-1 - pm) << lgT) + 8 * cj;
+            uint32_t cv[8];
+            bool any = false;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                cv[q] = canon_vr(ce[q]);
+                any |= cv[q] == 65536u;
+            }
+            store8(o, cv);
+            if (any && a.out_oor.counts)
+                for (int q = 0; q < 8; q++)
+                    if (cv[q] == 65536u)
+                        record(r, cw + q);
+        }
+        return;
+    }
+    if (!valid)
+        return;
+    for (int r = g; r < a.out_rows; r += G) {
+        const int t = a.out_first + r, pm = s_pos[t];
+        uint32_t cv;
+        if (pm >= 0) {
+            cv = row_ptr(src.by_pos ? pm : t)[cg];
+        } else {
+            cv = canon_vr(s_cE[((-1 - pm) << lgT) + col]);
+            if (cv == 65536u && a.out_oor.counts)
+                record(r, cg);
+        }
+        a.out[s * a.oss + r * a.ors + cg] = static_cast<uint16_t>(cv);
+    }
+}
+
 namespace {
 
 int ilog2i(long long v)
@@ -1039,9 +1375,11 @@ int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab, int* twi
     return off;
 }
 
-size_t lds_bytes(const qi_plan* p, int lgT, int tw_words, bool twg)
+// rows: the image's rows (nmax; n for the non-systematic encode, which
+// runs NTT_n alone)
+size_t lds_bytes(const qi_plan* p, int lgT, int tw_words, bool twg, int rows)
 {
-    return ((static_cast<size_t>(p->nmax) << lgT) +
+    return ((static_cast<size_t>(rows) << lgT) +
             lds_side_words(tw_words, p->k, p->len2k, twg)) *
            4;
 }
@@ -1066,16 +1404,16 @@ void lds_table_range(const qi_plan* p, int mode, int* lo, int* hi)
 // for two workgroups per CU with the tables staged, else with the tables
 // read from global memory (*twg), else one workgroup per CU (at least 8
 // columns)
-int lds_geom(const qi_plan* p, int tw_words, bool* twg)
+int lds_geom(const qi_plan* p, int tw_words, bool* twg, int rows)
 {
     for (int g = 0; g < 2; g++)
         for (int lg = 6; lg >= 3; lg--)
-            if (lds_bytes(p, lg, tw_words, g == 1) <= kLdsCap / 2) {
+            if (lds_bytes(p, lg, tw_words, g == 1, rows) <= kLdsCap / 2) {
                 *twg = g == 1;
                 return lg;
             }
     *twg = false;
-    return lds_bytes(p, 3, tw_words, false) <= kLdsCap ? 3 : -1;
+    return lds_bytes(p, 3, tw_words, false, rows) <= kLdsCap ? 3 : -1;
 }
 
 bool lds_engine(const qi_plan* p)
@@ -1085,7 +1423,95 @@ bool lds_engine(const qi_plan* p)
     int lo, hi;
     lds_table_range(p, kLdsSysDec, &lo, &hi);  // the largest set
     bool twg;
-    return lds_geom(p, hi - lo, &twg) >= 0;
+    return lds_geom(p, hi - lo, &twg, p->nmax) >= 0;
+}
+
+// ---- erasure decode (ntt_eras_kernel) ----
+bool eras_plan(const qi_plan* p)
+{
+    return p->ntt && !p->mbig && p->n <= kLdsMaxN && p->n - p->k <= kErasMax;
+}
+
+ErasCtxLayout eras_layout(const qi_plan* p)
+{
+    return ErasCtxLayout{p->k, p->n, p->n - p->k};
+}
+
+size_t eras_bytes(const qi_plan* p, int lgT, int tw_words, bool twg)
+{
+    const ErasCtxLayout L = eras_layout(p);
+    return ((static_cast<size_t>(p->n) << lgT) + (twg ? 0 : tw_words) + L.k + L.n + L.e +
+            static_cast<size_t>(L.e) * L.e + (static_cast<size_t>(L.e) << lgT)) *
+           4;
+}
+
+// INTT_n's tables only: [0, NTT_h's first table)
+int eras_tw_words(const qi_plan* p, XfPlan* pl)
+{
+    lds_tables(p, pl, nullptr);
+    return pl[kTwP2f].tw[0];
+}
+
+int eras_geom(const qi_plan* p, bool* twg)
+{
+    XfPlan pl[4];
+    const int tw_words = eras_tw_words(p, pl);
+    for (int g = 0; g < 2; g++)
+        for (int lg = 6; lg >= 3; lg--)
+            if (eras_bytes(p, lg, tw_words, g == 1) <= kLdsCap / 2) {
+                *twg = g == 1;
+                return lg;
+            }
+    *twg = false;
+    return eras_bytes(p, 3, tw_words, false) <= kLdsCap ? 3 : -1;
+}
+
+int eras_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
+{
+    a.k = p->k;
+    a.n = p->n;
+    a.len2k = p->len2k;
+    a.nmax = p->n;
+    XfPlan pl[4];
+    a.tw_words = eras_tw_words(p, pl);
+    a.pni = pl[kTwPni];
+    a.tw = p->d_ldstw;
+    bool twg;
+    a.lgT = eras_geom(p, &twg);
+    if (a.lgT < 0 || !a.tw)
+        return -3;
+    const ErasCtxLayout L = eras_layout(p);
+    a.ids_off = static_cast<int>(L.ids_off());
+    a.pos_off = static_cast<int>(L.pos_off());
+    a.eras_e = L.e;
+    a.eras_eid = static_cast<int>(L.eid_off());
+    a.eras_b = static_cast<int>(L.b_off());
+    a.inv_n = balanced(invmod_c(static_cast<uint32_t>(p->n)));
+    const long long tiles = (a.words + (1LL << a.lgT) - 1) >> a.lgT;
+    if (tiles * S > 0x7fffffffLL)
+        return -3;
+    a.tiles = static_cast<int>(tiles);
+    {
+        auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+        auto a8 = [](long long v) { return (v & 7) == 0; };
+        const RowSrc& r = a.src;
+        a.wide = (a.words & 7) == 0 && al(r.base0) && a8(r.ss0) && a8(r.rs0) &&
+                 (!r.base1 || (al(r.base1) && a8(r.ss1) && a8(r.rs1))) && al(a.out) &&
+                 a8(a.oss) && a8(a.ors);
+    }
+    const size_t lds = eras_bytes(p, a.lgT, a.tw_words, twg);
+    const void* fn = twg ? reinterpret_cast<const void*>(&ntt_eras_kernel<true>)
+                         : reinterpret_cast<const void*>(&ntt_eras_kernel<false>);
+    if (lds > 65536 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           static_cast<int>(lds)) != hipSuccess)
+        return -2;
+    if (twg)
+        hipLaunchKernelGGL(ntt_eras_kernel<true>, dim3(static_cast<unsigned>(tiles * S)),
+                           dim3(kLdsThreads), lds, st, a);
+    else
+        hipLaunchKernelGGL(ntt_eras_kernel<false>, dim3(static_cast<unsigned>(tiles * S)),
+                           dim3(kLdsThreads), lds, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
@@ -1109,8 +1535,12 @@ int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
     a.pnf = pl[kTwPnf];
     a.tw = p->d_ldstw + lo;
     a.tw_words = hi - lo;
+    // the non-systematic encode runs NTT_n alone: an n-row image (the side
+    // arrays start after it), so wider tiles where len_2k > n
+    if (a.mode == kLdsEnc)
+        a.nmax = p->n;
     bool twg;
-    a.lgT = lds_geom(p, a.tw_words, &twg);
+    a.lgT = lds_geom(p, a.tw_words, &twg, a.nmax);
     if (a.lgT < 0)
         return -3;
     const NttCtxLayout L = ctx_layout_of(p);
@@ -1129,7 +1559,7 @@ int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
                  (!r.base1 || (al(r.base1) && a8(r.ss1) && a8(r.rs1))) && al(a.out) &&
                  a8(a.oss) && a8(a.ors);
     }
-    const size_t lds = lds_bytes(p, a.lgT, a.tw_words, twg);
+    const size_t lds = lds_bytes(p, a.lgT, a.tw_words, twg, a.nmax);
     const void* fn = twg ? reinterpret_cast<const void*>(&ntt_lds_kernel<true>)
                          : reinterpret_cast<const void*>(&ntt_lds_kernel<false>);
     if (lds > 65536 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1215,7 +1645,7 @@ int interpolate(const qi_plan* p, const int32_t* ctx, long long cs, const RowSrc
 
 long long ntt_ctx_words(const qi_plan* p)
 {
-    return ctx_layout_of(p).words();
+    return eras_plan(p) ? eras_layout(p).words() : ctx_layout_of(p).words();
 }
 
 int ntt_build_ctx(const qi_plan* p, const uint16_t* d_ids, int S, int32_t* ctx, long long cs,
@@ -1223,6 +1653,12 @@ int ntt_build_ctx(const qi_plan* p, const uint16_t* d_ids, int S, int32_t* ctx, 
 {
     if (S <= 0)
         return 0;
+    if (eras_plan(p)) {
+        const uint32_t r = root_of_unity(static_cast<uint32_t>(p->n));
+        ErasCtxArgs e{eras_layout(p), r, invmod_c(r), d_ids, ctx, cs};
+        hipLaunchKernelGGL(eras_ctx_kernel, dim3(S), dim3(64), 0, st, e);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
     NttCtxArgs a{ctx_layout_of(p), p->r, root_of_unity(static_cast<uint32_t>(p->len2k)),
                  invmod_c(static_cast<uint32_t>(p->len2k)), d_ids, ctx, cs};
     const size_t lds =
@@ -1260,7 +1696,7 @@ int ntt_plan_init(qi_plan* p)
     p->d_tw[1] = d + p->nmax;
     if (hipMemcpy(d, tw.data(), tw.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return -2;
-    if (lds_engine(p)) {
+    if (lds_engine(p) || eras_plan(p)) {
         XfPlan pl[4];
         std::vector<int32_t> tab;
         lds_tables(p, pl, &tab);
@@ -1283,14 +1719,22 @@ int ntt_plan_init(qi_plan* p)
 
 std::string ntt_kernel_names(const qi_plan* p, bool decode)
 {
+    if (eras_plan(p) && (decode || p->sys)) {
+        bool twg;
+        (void)eras_geom(p, &twg);
+        return std::string(decode ? "eras_ctx_kernel + " : "") +
+               (twg ? "ntt_eras_kernel<true>" : "ntt_eras_kernel<false>");
+    }
     if (!lds_engine(p))
-        return decode ? "ntt_expand_kernel + ntt_fix_kernel + ntt_pass_kernel" : "ntt_pass_kernel";
+        return decode ? "ntt_ctx_kernel + ntt_expand_kernel + ntt_fix_kernel + ntt_pass_kernel"
+                      : "ntt_pass_kernel";
     const int mode = decode ? (p->sys ? kLdsSysDec : kLdsDec) : (p->sys ? kLdsSysEnc : kLdsEnc);
     int lo, hi;
     lds_table_range(p, mode, &lo, &hi);
     bool twg;
-    (void)lds_geom(p, hi - lo, &twg);
-    return twg ? "ntt_lds_kernel<true>" : "ntt_lds_kernel<false>";
+    (void)lds_geom(p, hi - lo, &twg, mode == kLdsEnc ? p->n : p->nmax);
+    return std::string(decode ? "ntt_ctx_kernel + " : "") +
+           (twg ? "ntt_lds_kernel<true>" : "ntt_lds_kernel<false>");
 }
 
 void ntt_plan_free(qi_plan* p)
@@ -1313,6 +1757,24 @@ int ntt_encode(const qi_plan* p, const uint16_t* data, long long dss, long long 
 {
     if (S <= 0 || words <= 0)
         return 0;
+    if (p->sys && eras_plan(p)) {
+        // the parities as the erased symbols of the data's codeword
+        NttLdsArgs a{};
+        a.mode = kLdsSysEnc;
+        a.words = words;
+        a.src = RowSrc{data, dss, drs, 1 << 30, nullptr, 0, 0, 1, p->k, 0};
+        a.ctx = p->d_sysctx;
+        a.cs = 0;
+        a.out = out.base;
+        a.oss = out.ss;
+        a.ors = out.rs;
+        a.out_first = p->k;
+        a.out_rows = p->n_outputs;
+        if (oor && oor->counts)
+            a.out_oor = *oor;
+        a.err = p->d_err;
+        return eras_launch(p, a, S, st);
+    }
     if (lds_engine(p)) {
         NttLdsArgs a{};
         a.mode = p->sys ? kLdsSysEnc : kLdsEnc;
@@ -1399,7 +1861,7 @@ int ntt_decode(const qi_plan* p, const int32_t* ctx, long long cs, RowSrc src,
 {
     if (S <= 0 || words <= 0)
         return 0;
-    if (lds_engine(p)) {
+    if (lds_engine(p) || eras_plan(p)) {
         NttLdsArgs a{};
         a.mode = p->sys ? kLdsSysDec : kLdsDec;
         a.words = words;
@@ -1415,7 +1877,7 @@ int ntt_decode(const qi_plan* p, const int32_t* ctx, long long cs, RowSrc src,
         a.out_first = 0;
         a.out_rows = p->k;
         a.err = p->d_err;
-        return lds_launch(p, a, S, st);
+        return eras_plan(p) ? eras_launch(p, a, S, st) : lds_launch(p, a, S, st);
     }
     const Slicing sl = slicing(p, words, S);
     const long long sss = static_cast<long long>(p->nmax) * sl.W;

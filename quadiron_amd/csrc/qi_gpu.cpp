@@ -277,7 +277,7 @@ const char* qi_gpu_kernels(const qi_plan* p, long long words)
     std::string enc, dec;
     if (!use_matrix(p, words)) {
         enc = ntt_kernel_names(p, false);
-        dec = "ntt_ctx_kernel + " + ntt_kernel_names(p, true);
+        dec = ntt_kernel_names(p, true);
     } else {
         if (p->ntt && !p->d_gen)
             enc = ntt_kernel_names(p, false);

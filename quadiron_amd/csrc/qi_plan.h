@@ -98,7 +98,8 @@ struct qi_plan {
 namespace qi {
 // ---- general-k path (ntt.hip) ----
 int ntt_plan_init(qi_plan* p);
-// the NTT engine's kernels for an encode or a decode: ntt_lds_kernel<TWG>
+// the NTT engine's kernels for an encode or a decode (a decode's list starts
+// with its context builder): ntt_eras_kernel<TWG> (few erasures), ntt_lds_kernel<TWG>
 // (max(n, len_2k) <= 2048) or the multi-pass engine
 std::string ntt_kernel_names(const qi_plan* p, bool decode);
 void ntt_plan_free(qi_plan* p);

@@ -242,6 +242,12 @@ def main():
     gen_blocks(ref, ora, "blk_k300_m212_w1024", 300, 212, 0, 256, 2048, 43, 2, 8, out)
     gen_blocks(ref, ora, "blk_k384_m128_sys_w1024", 384, 128, 1, 512, 2048, 44, 2, 8,
                out)
+    # few erasures (n - k <= 64): the erasure decode of the NTT engine (round
+    # 4) -- n = 1024 and 512, systematic, and n = 2048 (len_2k = 4096: the
+    # encode on the multi-pass engine)
+    gen_blocks(ref, ora, "blk_k1000_m24", 1000, 24, 0, 64, 256 + 6, 45, 2, 8, out)
+    gen_blocks(ref, ora, "blk_k500_m12_sys", 500, 12, 1, 128, 512, 46, 2, 8, out)
+    gen_blocks(ref, ora, "blk_k2000_m48", 2000, 48, 0, 32, 128 + 2, 47, 2, 8, out)
 
 
 if __name__ == "__main__":

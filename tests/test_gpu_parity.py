@@ -331,6 +331,14 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True,
     (1000, 24, 1, 1, 512),
     (600, 1400, 0, 1, 256),   # n = len_2k = 2048: no free image rows
     (385, 127, 0, 2, 1032),   # smallest k past the matrix path
+    # few erasures (n - k <= 64): the erasure decode (and the systematic
+    # encode as the same solve): n = 512 / 1024 / 2048, e = 4 .. 64
+    (450, 62, 0, 2, 1024),
+    (448, 64, 1, 2, 1000),
+    (500, 12, 1, 2, 1000),
+    (1020, 4, 0, 2, 333),
+    (2000, 48, 0, 1, 520),    # len_2k = 4096: encode on the multi-pass engine
+    (1990, 58, 1, 1, 256),
 ])
 def test_batch_vs_oracle(k, m, sys_, S, P):
     _batch_roundtrip(k, m, sys_, S, P, seed=k * 1000 + m + P, n_craft=16)

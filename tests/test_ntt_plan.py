@@ -194,3 +194,57 @@ def test_decode_pipeline(k, m, split):
     w2i = pow(w2, Q - 2, Q)
     y = [(out[0][t] + pow(w2i, t, Q) * out[1][t]) % Q for t in range(k)]
     assert y == coef
+
+
+# ---------------------------------------------------------------------------
+# Erasure decode (ntt.hip, plans with e = n - k <= kErasMax): instead of
+# decode_apply's INTT_n -> NTT_2k -> x C -> INTT_2k, the e erased codeword
+# symbols are solved from the e "syndromes" the zero-filled codeword leaves
+# in the top INTT outputs, then one more INTT_n (non-systematic) or nothing
+# (systematic: the data ARE codeword symbols).  The codeword of both types is
+# c_j = P(r^j), deg P < k, j < n (positions >= k + m are never sent).
+
+def _lagrange_rows(xs):
+    """W[j][u] = coef_u(L_j), L_j = prod_{l != j} (X - x_l) / (x_j - x_l)."""
+    e = len(xs)
+    A = [1]  # prod (X - x_l), coefficients low to high
+    for x in xs:
+        A = [(a_lo - x * a) % Q for a, a_lo in zip(A + [0], [0] + A)]
+    W = []
+    for xj in xs:
+        q = [0] * e  # Q_j = A / (X - xj) by synthetic division from the top
+        q[e - 1] = 1
+        for t in range(e - 1, 0, -1):
+            q[t - 1] = (A[t] + xj * q[t]) % Q
+        ap = 0
+        for t in range(e - 1, -1, -1):
+            ap = (ap * xj + q[t]) % Q
+        inv = pow(ap, Q - 2, Q)
+        W.append([v * inv % Q for v in q])
+    return W
+
+
+@pytest.mark.parametrize("n,k,sys_", [(16, 11, 0), (64, 50, 0), (64, 50, 1), (32, 31, 1),
+                                      (128, 100, 0)])
+def test_erasure_decode_math(n, k, sys_):
+    rng = random.Random(n * 7 + k + sys_)
+    r, ri = root(n), pow(root(n), Q - 2, Q)
+    P = [rng.randrange(Q) for _ in range(k)]
+    c = [sum(P[t] * pow(r, j * t, Q) for t in range(k)) % Q for j in range(n)]
+    recv = sorted(rng.sample(range(n), k))
+    E = [j for j in range(n) if j not in recv]
+    e = len(E)
+    # y' = unnormalised INTT_n of the zero-filled codeword
+    cz = [c[j] if j in recv else 0 for j in range(n)]
+    y = [sum(cz[j] * pow(ri, j * t, Q) for j in range(n)) % Q for t in range(n)]
+    # per-pattern constants: B[j][u] = -r^(E_j k) W[j][u], x_j = r^-E_j
+    W = _lagrange_rows([pow(ri, j, Q) for j in E])
+    B = [[(-pow(r, E[a] * k, Q) * W[a][u]) % Q for u in range(e)] for a in range(e)]
+    cE = [sum(B[a][u] * y[k + u] for u in range(e)) % Q for a in range(e)]
+    assert cE == [c[j] for j in E]
+    if sys_:
+        return  # the data rows c_t, t < k: received or in cE
+    full = [cz[j] if j in recv else cE[E.index(j)] for j in range(n)]
+    ninv = pow(n, Q - 2, Q)
+    d = [sum(full[j] * pow(ri, j * t, Q) for j in range(n)) * ninv % Q for t in range(k)]
+    assert d == P
