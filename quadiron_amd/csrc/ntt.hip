@@ -1535,9 +1535,14 @@ int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
     a.pnf = pl[kTwPnf];
     a.tw = p->d_ldstw + lo;
     a.tw_words = hi - lo;
-    // the non-systematic encode runs NTT_n alone: an n-row image (the side
-    // arrays start after it), so wider tiles where len_2k > n
-    if (a.mode == kLdsEnc)
+    // the non-systematic encode runs NTT_n alone and could take an n-row
+    // image (wider tiles where len_2k > n); measured slower at k1000 (T = 16
+    // instead of 8: encode 1.27-1.29 -> 1.33 ms, gpurun_out ab_route), so the
+    // image stays nmax rows (QI_ENC_NIMG=1: the n-row variant)
+#ifndef QI_ENC_NIMG
+#define QI_ENC_NIMG 0
+#endif
+    if (QI_ENC_NIMG && a.mode == kLdsEnc)
         a.nmax = p->n;
     bool twg;
     a.lgT = lds_geom(p, a.tw_words, &twg, a.nmax);
@@ -1732,7 +1737,7 @@ std::string ntt_kernel_names(const qi_plan* p, bool decode)
     int lo, hi;
     lds_table_range(p, mode, &lo, &hi);
     bool twg;
-    (void)lds_geom(p, hi - lo, &twg, mode == kLdsEnc ? p->n : p->nmax);
+    (void)lds_geom(p, hi - lo, &twg, QI_ENC_NIMG && mode == kLdsEnc ? p->n : p->nmax);
     return std::string(decode ? "ntt_ctx_kernel + " : "") +
            (twg ? "ntt_lds_kernel<true>" : "ntt_lds_kernel<false>");
 }
