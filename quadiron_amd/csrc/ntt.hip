@@ -471,6 +471,7 @@ struct NttLdsArgs {
     // the e x e solve in the context, n^-1 (balanced)
     int eras_e, eras_eid, eras_b;
     int32_t inv_n;
+    const int32_t* rinv;  // w_R^-x, x < R = 2^pni.lgr[0] (d_ldstw tail)
 };
 
 // One pass over the image: tasks (group start b, offset j < s) of the R
@@ -863,6 +864,71 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     }
 }
 
+// INTT_n (DIT, as lds_transform<false, true>) computing only the outputs
+// t >= k (the erasure decode's syndromes): every pass but the last as usual,
+// then the last pass (q = 0: tasks j < s, positions j + u s) evaluates just
+// the outputs u >= ceil((k - j) / s) of its R-point inverse DFT directly
+// (y_u = sum_q v'_q w_R^-qu with the twiddled inputs v'; a handful per task)
+// instead of the whole codelet.  rinv: w_R^-x, x < R, balanced (R = 2^lgr[0]).
+__device__ void lds_intt_top(int32_t* buf, const int32_t* tw, const XfPlan& P, int lgT, int col,
+                             int g, int G, int k, const int32_t* rinv)
+{
+    for (int i = 0; i + 1 < P.np; i++) {
+        const int q = P.np - 1 - i;
+        const int lgs = P.sh[q], lgL = lgs + P.lgr[q];
+        const int32_t* twp = tw + P.tw[q];
+        switch (P.lgr[q]) {
+        case 1:
+            lds_pass<2, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, nullptr, 0,
+                                            &P, 0);
+            break;
+        case 2:
+            lds_pass<4, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, nullptr, 0,
+                                            &P, 0);
+            break;
+        case 3:
+            lds_pass<8, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, nullptr, 0,
+                                            &P, 0);
+            break;
+        case 4:
+            lds_pass<16, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, nullptr,
+                                             0, &P, 0);
+            break;
+        default:
+            lds_pass<32, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, nullptr,
+                                             0, &P, 0);
+            break;
+        }
+        __syncthreads();
+    }
+    const int lgR = P.lgr[0], R = 1 << lgR, lgs = P.sh[0], sN = 1 << lgs;
+    const int32_t* twp = tw + P.tw[0];
+    for (int j = g; j < sN; j += G) {
+        const int umin = k > j ? (k - j + sN - 1) >> lgs : 0;
+        if (umin >= R)
+            continue;
+        const int lb = (j << lgT) + col;
+        int32_t v[32];
+#pragma unroll
+        for (int q = 0; q < 32; q++) {
+            if (q < R) {
+                v[q] = buf[lb + ((q << lgs) << lgT)];
+                if (q > 0 && lgs > 0)
+                    v[q] = mul_rt(v[q], twp[j * R + q]);
+            }
+        }
+        for (int u = umin; u < R; u++) {
+            int32_t acc = v[0];  // |acc| <= 32 * 65540
+#pragma unroll
+            for (int q = 1; q < 32; q++)
+                if (q < R)
+                    acc += mul_rt(v[q], rinv[(q * u) & (R - 1)]);
+            buf[lb + ((u << lgs) << lgT)] = fold(fold(acc));
+        }
+    }
+    __syncthreads();
+}
+
 // ---------------------------------------------------------------------------
 // Erasure decode (plans with few erasures: e = n - k <= kErasMax, n <= 2048,
 // eras_plan).  The codeword of both types is c_j = P(r^j), deg P < k, over
@@ -993,6 +1059,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
     int32_t* s_eid = s_pos + n;
     int32_t* s_B = s_eid + e;
     int32_t* s_cE = s_B + e * e;
+    int32_t* s_rinv = s_cE + (e << lgT);  // w_R^-x of INTT_n's last pass
     int b = blockIdx.x;  // XCD-contiguous tiles, as ntt_lds_kernel
     if ((gridDim.x & 7) == 0)
         b = (b & 7) * static_cast<int>(gridDim.x >> 3) + (b >> 3);
@@ -1013,6 +1080,8 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
         s_eid[j] = ctx[a.eras_eid + j];
     for (int i = tid; i < e * e; i += kLdsThreads)
         s_B[i] = ctx[a.eras_b + i];
+    if (tid < (1 << a.pni.lgr[0]))
+        s_rinv[tid] = a.rinv[tid];
     __syncthreads();
     const RowSrc& src = a.src;
     auto row_ptr = [&](int id) {
@@ -1099,7 +1168,8 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
         }
     };
     load(false);
-    lds_transform<false, true>(buf, tw, a.pni, lgT, col, g, G);
+    // only the syndromes y'_[k, n) are needed from this transform
+    lds_intt_top(buf, tw, a.pni, lgT, col, g, G, k, s_rinv);
     // c_E = B y'_[k, n): e lazy products per (erasure, column) item
     for (int it = tid; it < (e << lgT); it += kLdsThreads) {
         const int j = it >> lgT, c = it & (T - 1);
@@ -1329,7 +1399,8 @@ XfPlan xf_plan(int N)
 // non-systematic encode the last one, systematic codes all four.
 enum : int { kTwPni = 0, kTwP2f = 1, kTwP2i = 2, kTwPnf = 3 };
 
-int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab, int* twist = nullptr)
+int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab, int* twist = nullptr,
+               int* rinv_off = nullptr)
 {
     const uint32_t w = root_of_unity(static_cast<uint32_t>(p->nmax));
     const int h = p->len2k / 2;
@@ -1370,6 +1441,18 @@ int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab, int* twi
             off += (L + 3) & ~3;
         }
     }
+    // the inverse R-th roots of INTT_n's last DIT pass (R = its pass-0
+    // radix) for the erasure decode's pruned last pass (lds_intt_top)
+    if (rinv_off)
+        *rinv_off = off;
+    if (tab) {
+        const int R = 1 << pl[kTwPni].lgr[0];
+        tab->resize(off + 32);
+        const uint32_t wi = invmod_c(root_of_unity(static_cast<uint32_t>(R)));
+        for (int x = 0; x < 32; x++)
+            (*tab)[off + x] = x < R ? balanced(powmod_c(wi, static_cast<uint32_t>(x))) : 0;
+    }
+    off += 32;
     if (tab)
         tab->resize(off);
     return off;
@@ -1441,7 +1524,7 @@ size_t eras_bytes(const qi_plan* p, int lgT, int tw_words, bool twg)
 {
     const ErasCtxLayout L = eras_layout(p);
     return ((static_cast<size_t>(p->n) << lgT) + (twg ? 0 : tw_words) + L.k + L.n + L.e +
-            static_cast<size_t>(L.e) * L.e + (static_cast<size_t>(L.e) << lgT)) *
+            static_cast<size_t>(L.e) * L.e + (static_cast<size_t>(L.e) << lgT) + 32) *
            4;
 }
 
@@ -1476,6 +1559,9 @@ int eras_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
     a.tw_words = eras_tw_words(p, pl);
     a.pni = pl[kTwPni];
     a.tw = p->d_ldstw;
+    int rinv_off = 0;
+    lds_tables(p, pl, nullptr, nullptr, &rinv_off);
+    a.rinv = p->d_ldstw ? p->d_ldstw + rinv_off : nullptr;
     bool twg;
     a.lgT = eras_geom(p, &twg);
     if (a.lgT < 0 || !a.tw)
