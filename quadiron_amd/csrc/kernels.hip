@@ -1049,6 +1049,15 @@ typedef int qi_v4i __attribute__((ext_vector_type(4)));
 // with this one's epilogue (cfg3 encode 1.078 -> 1.063 ms; at KS = 2 the
 // second accumulator set cost occupancy: k32 decode 0.83 -> 0.99 ms)
 static constexpr bool kMmPipe = true;
+// the tall KS = 4 generators (cfg3's 1024 x 64 encode): super tiles per
+// block and whether the pipelined pair loop runs (A/B knobs)
+#ifndef QI_ENC4_NST
+#define QI_ENC4_NST 8
+#endif
+#ifndef QI_ENC4_PIPE
+#define QI_ENC4_PIPE 1
+#endif
+static constexpr int kEnc4Nst = QI_ENC4_NST;
 typedef int qi_v2i __attribute__((ext_vector_type(2)));
 typedef unsigned int qi_v4u __attribute__((ext_vector_type(4)));
 
@@ -1477,7 +1486,7 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             __builtin_amdgcn_wave_barrier();
         };
         auto st_of = [&](int st) { return rsplit ? st : wv * nst + st; };
-        if constexpr (kMmPipe && KS == 4 && nst >= 2 && nst % 2 == 0) {
+        if constexpr (kMmPipe && QI_ENC4_PIPE && KS == 4 && nst >= 2 && nst % 2 == 0) {
             // software pipeline over super-tile pairs: the MFMAs of tile
             // st + 1 are issued between the element math of tile st (two
             // accumulator sets), interleaved by sched_group_barrier so the
@@ -2321,6 +2330,7 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
             return os_launch<KS, 8, 1>(a, wfull, S, st);
     }
     constexpr int NSTS = KS == 1 ? 16 : 8;
+    constexpr int NSTG = KS == 4 ? kEnc4Nst : NSTS;  // tall generators
     const int RB = a.L.RB();
     if constexpr (KS > 16) {
         return -1;  // only the operand-stationary kernel takes kin > 256
@@ -2339,7 +2349,7 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
         return mfma_launch<KS, 4, 4, true>(a, wfull, S, st);
     } else {
         if (RB >= 4)
-            return mfma_launch<KS, NSTS, 4, true>(a, wfull, S, st);
+            return mfma_launch<KS, NSTG, 4, true>(a, wfull, S, st);
         return mfma_launch<KS, NSTS, 4, false>(a, wfull, S, st);
     }
 }
@@ -2433,6 +2443,8 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
         const int RB = L.RB();
         int nst = KS == 1 ? 16 : 8, nw = 4;
         bool rsplit = RB >= 4;
+        if (KS == 4 && rsplit)
+            nst = kEnc4Nst;
         if (KS == 16) {
             nst = 1;
             rsplit = true;
