@@ -1050,7 +1050,10 @@ typedef int qi_v4i __attribute__((ext_vector_type(4)));
 // second accumulator set cost occupancy: k32 decode 0.83 -> 0.99 ms)
 static constexpr bool kMmPipe = true;
 // the tall KS = 4 generators (cfg3's 1024 x 64 encode): super tiles per
-// block and whether the pipelined pair loop runs (A/B knobs)
+// block and whether the pipelined pair loop runs (A/B knobs).  Smaller
+// blocks buy occupancy (125 VGPRs without the pair loop) and lose: cfg3
+// encode 1.05 ms at 8 super tiles + pairs (2 waves/SIMD), 1.06 without the
+// pairs, 1.16 at 4 (3 blocks per CU), 1.37 at 2 (gpurun_out ab_geo)
 #ifndef QI_ENC4_NST
 #define QI_ENC4_NST 8
 #endif
