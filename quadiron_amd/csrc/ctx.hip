@@ -195,6 +195,115 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
     }
 }
 
+// The BIG contexts' packing for whole-tile widths (see decode_ctx_kernel):
+// rows t of Mt (canonical coef_t(Q_i), pitch kp, global memory) scaled by
+// the columns' 1 / A'(x_i), row-scaled when an entry breaks coef_ok (as
+// pack_row_grp: the row's scale search on its 32-lane group), summed into
+// kcorr / kmf, and written as the [a | 0], [0 | b], [b | a] operand tiles.
+template <int NT>
+__device__ void pack_tiles_direct(const uint32_t* Mt, int kp, const uint32_t* cinv,
+                                  const MatLayout& L, int32_t* mat)
+{
+    constexpr int LPR = 32, ROWS = NT / LPR;  // 32 rows (two row blocks) per pass
+    constexpr int MM = (kMatMaxKin / 4 + LPR - 1) / LPR;
+    constexpr int NJ = kMatMaxKin / 4;  // 4-entry groups per row, at most
+    __shared__ uint32_t stg[ROWS][2 * NJ];  // per row: (aw, bw) of each group
+    const int k = L.kin, KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
+    const int tid = threadIdx.x, sub = tid % LPR, rl = tid / LPR;
+    int32_t* mf = mat + L.mf();
+    for (int rb0 = 0; rb0 < RB; rb0 += ROWS / 16) {
+        const int t = 16 * rb0 + rl;
+        if (t < L.R) {
+            uint32_t v[MM][4];
+            uint32_t bad = 0;
+#pragma unroll
+            for (int m = 0; m < MM; m++)
+#pragma unroll
+                for (int jb = 0; jb < 4; jb++) {
+                    const int i = 4 * (sub + m * LPR) + jb;
+                    v[m][jb] = i < k ? mulm(Mt[static_cast<size_t>(t) * kp + i], cinv[i]) : 0u;
+                    bad |= i < k && !coef_ok(balanced(v[m][jb]));
+                }
+            bad = grp_or(bad, LPR);
+            uint32_t sc = 1;
+            while (bad) {  // rare; uniform in the group
+                sc++;
+                const int32_t si = balanced(powm(sc, 65535u));
+                if (iabs32(si) > 32766)
+                    continue;
+                bad = 0;
+#pragma unroll
+                for (int m = 0; m < MM; m++)
+#pragma unroll
+                    for (int jb = 0; jb < 4; jb++) {
+                        const int i = 4 * (sub + m * LPR) + jb;
+                        bad |= i < k && !coef_ok(balanced(mulm(v[m][jb], sc)));
+                    }
+                bad = grp_or(bad, LPR);
+            }
+            uint32_t sum = 0;
+#pragma unroll
+            for (int m = 0; m < MM; m++) {
+                uint32_t aw = 0, bw = 0;
+#pragma unroll
+                for (int jb = 0; jb < 4; jb++) {
+                    const int i = 4 * (sub + m * LPR) + jb;
+                    if (i < k) {
+                        const uint32_t c = sc == 1 ? v[m][jb] : mulm(v[m][jb], sc);
+                        sum += c;
+                        int32_t a, b;
+                        split_i8(c, a, b);
+                        aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
+                        bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
+                    }
+                }
+                const int jg = sub + m * LPR;
+                if (jg < nj) {
+                    stg[rl][2 * jg] = aw;
+                    stg[rl][2 * jg + 1] = bw;
+                }
+            }
+            sum = grp_add(sum, LPR);
+            if (sub == 0) {
+                int32_t f = static_cast<int32_t>(sum & 0xffffu) - static_cast<int32_t>(sum >> 16);
+                f = f < 0 ? f + 65537 : f;
+                const uint32_t sq = static_cast<uint32_t>(f >= 65537 ? f - 65537 : f);
+                mat[L.kcorr() + t] = static_cast<int32_t>(mulm(sq, 32768u));
+                const int32_t rs = sc == 1 ? 1 : balanced(powm(sc, 65535u));
+                mat[L.rscale() + t] = rs;
+                mat[L.kmf() + t] = static_cast<int32_t>(mulm(sq, 32896u));
+                mat[L.rscale_mf() + t] = rs;
+            }
+        } else {
+            for (int jg = sub; jg < nj; jg += LPR)
+                stg[rl][2 * jg] = stg[rl][2 * jg + 1] = 0;
+        }
+        __syncthreads();
+        // the two row blocks' tile dwords, rows fastest (whole 128-byte tile
+        // lines per wave store); zero halves of [a | 0] / [0 | b] not written
+        // at KS >= 4 (never read)
+        const int nrb = min(ROWS / 16, RB - rb0);
+        for (int it = tid; it < nrb * nj * 16; it += NT) {
+            const int tl = it & 15, jj = it >> 4;
+            const int jg = jj % nj, rbl = jj / nj, rb = rb0 + rbl;
+            const uint32_t aw = stg[16 * rbl + tl][2 * jg], bw = stg[16 * rbl + tl][2 * jg + 1];
+#pragma unroll
+            for (int half = 0; half < 2; half++) {
+                const int K = half * KH + 4 * jg;
+                const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
+                const size_t base =
+                    static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl) * 2 + dw;
+                if (KS < 4 || half == 0)
+                    mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
+                if (KS < 4 || half == 1)
+                    mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
+                mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // LDS row pitch of the context kernel's k x k matrix: 4 x odd, >= k
 __host__ __device__ inline int ctx_pitch(int k)
 {
@@ -373,6 +482,16 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         }
     }
     __syncthreads();
+    if (BIG && !dot2) {
+        // whole-tile widths: the operand tiles straight from the rows, two
+        // 16-row blocks at a time (32 lanes per row, 4 consecutive entries
+        // per lane and group: scale, split, staged in LDS, then stored
+        // rows-fastest as whole tile lines) -- no `plain` write-back, no
+        // re-read of the rows, no dot2 section (the kernels take single
+        // coefficients from the tiles)
+        pack_tiles_direct<NT>(Mt, kp, cinv, L, mat);
+        return;
+    }
     {
         // LPR lanes per row: 4 entries per lane at k = 64
         // (16 entries per lane: lpr = 32 covers k <= 512)

@@ -475,6 +475,8 @@ def test_cfg3_random_patterns_vs_oracle():
     (64, 960, 96, 1024),    # ~27 %
     (100, 28, 48, 1024),    # KS = 8
     (128, 128, 24, 1024),
+    (200, 56, 24, 1024),    # the BIG context packed straight into the tiles
+    (256, 768, 8, 2048),
 ])
 def test_decode_row_scales_many_stripes(k, m, S, P):
     """Many random erasure patterns: the decode contexts whose interpolation
