@@ -1060,7 +1060,11 @@ static constexpr bool kMmPipe = true;
 #ifndef QI_ENC4_PIPE
 #define QI_ENC4_PIPE 1
 #endif
+#ifndef QI_ENC4_NW
+#define QI_ENC4_NW 4
+#endif
 static constexpr int kEnc4Nst = QI_ENC4_NST;
+static constexpr int kEnc4Nw = QI_ENC4_NW;
 typedef int qi_v2i __attribute__((ext_vector_type(2)));
 typedef unsigned int qi_v4u __attribute__((ext_vector_type(4)));
 
@@ -1312,7 +1316,6 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
                        const int32_t rs, const int32_t (&pr)[3]) {
         const int t = 16 * rb + tl;
         const bool trow = t < L.R;
-        const int tcl = trow ? t : L.R - 1;  // a valid row for the loads
         // MFMAs of super tile ST into acc
         auto tile_mfma = [&](const int ST, qi_v4i (&acc)[4][3]) {
 #pragma unroll
@@ -1837,7 +1840,6 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         auto* lds = (__attribute__((address_space(3))) const uint8_t*)img;
         const int t = 16 * rbj[j] + tl;
         const bool trow = act[j] && t < L.R;
-        const int tcl = t < L.R ? t : L.R - 1;
         qi_v4i acc[4][3];
 #pragma unroll
         for (int T = 0; T < 4; T++) {
@@ -2262,7 +2264,11 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
         return -1;
     const int RB = a.L.RB();
     const int G = (RB + WR * RPW - 1) / (WR * RPW);
-    long long C = (512 + static_cast<long long>(S) * G - 1) / (static_cast<long long>(S) * G);
+    // blocks wanted over the launch: ~2 per CU, or ~8 for the short KS = 4
+    // decodes (cfg3: two column ranges per stripe, 0.168 -> 0.158 ms; the
+    // KS >= 8 decodes and generators lose at 2048, gpurun_out ab_x4)
+    constexpr long long kTarget = KS == 4 ? 2048 : 512;
+    long long C = (kTarget + static_cast<long long>(S) * G - 1) / (static_cast<long long>(S) * G);
     C = std::max(1LL, std::min(C, std::max(1LL, TS / 4)));
     // the XCD map wants S * C a multiple of 8
     while ((S * C) % 8 != 0 && C < TS / 2)
@@ -2352,7 +2358,7 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
         return mfma_launch<KS, 4, 4, true>(a, wfull, S, st);
     } else {
         if (RB >= 4)
-            return mfma_launch<KS, NSTG, 4, true>(a, wfull, S, st);
+            return mfma_launch<KS, NSTG, KS == 4 ? kEnc4Nw : 4, true>(a, wfull, S, st);
         return mfma_launch<KS, NSTS, 4, false>(a, wfull, S, st);
     }
 }
@@ -2446,8 +2452,10 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
         const int RB = L.RB();
         int nst = KS == 1 ? 16 : 8, nw = 4;
         bool rsplit = RB >= 4;
-        if (KS == 4 && rsplit)
+        if (KS == 4 && rsplit) {
             nst = kEnc4Nst;
+            nw = kEnc4Nw;
+        }
         if (KS == 16) {
             nst = 1;
             rsplit = true;

@@ -870,8 +870,11 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
 // the outputs u >= ceil((k - j) / s) of its R-point inverse DFT directly
 // (y_u = sum_q v'_q w_R^-qu with the twiddled inputs v'; a handful per task)
 // instead of the whole codelet.  rinv: w_R^-x, x < R, balanced (R = 2^lgr[0]).
+// With syn (e x T, row t - k) the outputs go there and the image keeps the
+// state after the other passes (the two-pass decode completes the transform
+// from it); otherwise into the image rows t.
 __device__ void lds_intt_top(int32_t* buf, const int32_t* tw, const XfPlan& P, int lgT, int col,
-                             int g, int G, int k, const int32_t* rinv)
+                             int g, int G, int k, const int32_t* rinv, int32_t* syn)
 {
     for (int i = 0; i + 1 < P.np; i++) {
         const int q = P.np - 1 - i;
@@ -923,7 +926,12 @@ __device__ void lds_intt_top(int32_t* buf, const int32_t* tw, const XfPlan& P, i
             for (int q = 1; q < 32; q++)
                 if (q < R)
                     acc += mul_rt(v[q], rinv[(q * u) & (R - 1)]);
-            buf[lb + ((u << lgs) << lgT)] = fold(fold(acc));
+            // output t = j + u s >= k: into syn (row t - k) when given,
+            // leaving the image as the passes before the last left it
+            if (syn)
+                syn[(((j + (u << lgs)) - k) << lgT) + col] = fold(fold(acc));
+            else
+                buf[lb + ((u << lgs) << lgT)] = fold(fold(acc));
         }
     }
     __syncthreads();
@@ -1046,7 +1054,11 @@ __global__ __launch_bounds__(64) void eras_ctx_kernel(ErasCtxArgs a)
 // The erasure decode of a tile of T columns of one stripe (and the
 // systematic encode, E = [k, n)), in LDS: image n x T, then the tables
 // (unless TWG), ids, the position map, E, B and c_E (e x T).
-template <bool TWG>
+// C2: the non-systematic decode of a two-pass INTT_n (np = 2), completed
+// from the image (see below); otherwise the second load + INTT_n.  Separate
+// instantiations: one kernel holding both completions kept more registers
+// live (150 VGPRs, 3 waves per SIMD: one 512-thread block per CU).
+template <bool TWG, bool C2>
 __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
 {
     extern __shared__ int32_t qi_ntt_lds[];
@@ -1060,6 +1072,9 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
     int32_t* s_B = s_eid + e;
     int32_t* s_cE = s_B + e * e;
     int32_t* s_rinv = s_cE + (e << lgT);  // w_R^-x of INTT_n's last pass
+    // C2: the syndromes y'_[k, n) (e x T <= n words, eras_launch) in the
+    // position map's place (a non-systematic decode reads it no more)
+    int32_t* s_syn = C2 ? s_pos : nullptr;
     int b = blockIdx.x;  // XCD-contiguous tiles, as ntt_lds_kernel
     if ((gridDim.x & 7) == 0)
         b = (b & 7) * static_cast<int>(gridDim.x >> 3) + (b >> 3);
@@ -1169,14 +1184,14 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
     };
     load(false);
     // only the syndromes y'_[k, n) are needed from this transform
-    lds_intt_top(buf, tw, a.pni, lgT, col, g, G, k, s_rinv);
+    lds_intt_top(buf, tw, a.pni, lgT, col, g, G, k, s_rinv, s_syn);
     // c_E = B y'_[k, n): e lazy products per (erasure, column) item
     for (int it = tid; it < (e << lgT); it += kLdsThreads) {
         const int j = it >> lgT, c = it & (T - 1);
         const int32_t* Bj = s_B + j * e;
         int32_t acc = 0;  // |acc| <= 64 * 65536
         for (int u = 0; u < e; u++)
-            acc += mul_rt(buf[((k + u) << lgT) + c], Bj[u]);
+            acc += mul_rt(C2 ? s_syn[(u << lgT) + c] : buf[((k + u) << lgT) + c], Bj[u]);
         s_cE[it] = fold(fold(acc));  // [-1, 65536]
     }
     __syncthreads();
@@ -1196,8 +1211,57 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
     };
     if (a.mode == kLdsDec) {
         // the completed codeword -> INTT_n -> the k coefficients (x n^-1)
-        load(true);
-        lds_transform<false, true>(buf, tw, a.pni, lgT, col, g, G);
+        const XfPlan& P = a.pni;
+        if constexpr (C2) {
+            // By linearity, INTT_n's first (unit) pass of the completed
+            // codeword is the image (that pass of the zero-filled one) plus
+            // its response to c_E: erased symbol t sits at element
+            // q0 = t >> lgr[0] of group t & (R0 - 1), and that group's
+            // output u gains c_E w_R1^(-q0 u).  Then only the last pass
+            // runs -- no second load of the received rows, no second unit
+            // pass.  Thread (u, c) owns output u of every group in column c,
+            // so erasures sharing a group add in turn.
+            const int lg0 = P.lgr[0], lg1 = P.lgr[1], m0 = (1 << lg0) - 1;
+            for (int it = tid; it < (1 << (lg1 + lgT)); it += kLdsThreads) {
+                const int u = it >> lgT, c = it & (T - 1);
+                for (int j = 0; j < e; j++) {
+                    const int t = s_eid[j], q0 = t >> lg0;
+                    int32_t* d = buf + ((((t & m0) << lg1) + u) << lgT) + c;
+                    // w_R1^-x = w_R0^(-x R0 / R1)
+                    const int32_t w = s_rinv[((q0 * u) << (lg0 - lg1)) & m0];
+                    *d = fold(fold(*d + mul_rt(s_cE[(j << lgT) + c], w)));
+                }
+            }
+            __syncthreads();
+            const int lgs = P.sh[0], lgL = lgs + lg0;
+            const int32_t* twp = tw + P.tw[0];
+            switch (lg0) {
+            case 1:
+                lds_pass<2, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, nullptr,
+                                                0, &P, 0);
+                break;
+            case 2:
+                lds_pass<4, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, nullptr,
+                                                0, &P, 0);
+                break;
+            case 3:
+                lds_pass<8, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G, nullptr,
+                                                0, &P, 0);
+                break;
+            case 4:
+                lds_pass<16, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G,
+                                                 nullptr, 0, &P, 0);
+                break;
+            default:
+                lds_pass<32, false, true, false>(buf, twp, P.N, lgs, lgL, lgT, col, g, G,
+                                                 nullptr, 0, &P, 0);
+                break;
+            }
+            __syncthreads();
+        } else {
+            load(true);
+            lds_transform<false, true>(buf, tw, P, lgT, col, g, G);
+        }
         if (a.wide) {
             if (!wvalid)
                 return;
@@ -1510,6 +1574,13 @@ bool lds_engine(const qi_plan* p)
 }
 
 // ---- erasure decode (ntt_eras_kernel) ----
+// the two-pass completion (ntt_eras_kernel<., true>): INTT_n in two passes
+// and the syndromes (e x T) fit the position map's n words
+static bool eras_c2(const XfPlan& pni, int e, int lgT)
+{
+    return pni.np == 2 && (static_cast<long long>(e) << lgT) <= pni.N;
+}
+
 bool eras_plan(const qi_plan* p)
 {
     return p->ntt && !p->mbig && p->n <= kLdsMaxN && p->n - p->k <= kErasMax;
@@ -1586,17 +1657,25 @@ int eras_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
                  a8(a.oss) && a8(a.ors);
     }
     const size_t lds = eras_bytes(p, a.lgT, a.tw_words, twg);
-    const void* fn = twg ? reinterpret_cast<const void*>(&ntt_eras_kernel<true>)
-                         : reinterpret_cast<const void*>(&ntt_eras_kernel<false>);
+    const bool c2 = a.mode == kLdsDec && eras_c2(a.pni, L.e, a.lgT);
+    const void* fn =
+        twg ? (c2 ? reinterpret_cast<const void*>(&ntt_eras_kernel<true, true>)
+                  : reinterpret_cast<const void*>(&ntt_eras_kernel<true, false>))
+            : (c2 ? reinterpret_cast<const void*>(&ntt_eras_kernel<false, true>)
+                  : reinterpret_cast<const void*>(&ntt_eras_kernel<false, false>));
     if (lds > 65536 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            static_cast<int>(lds)) != hipSuccess)
         return -2;
-    if (twg)
-        hipLaunchKernelGGL(ntt_eras_kernel<true>, dim3(static_cast<unsigned>(tiles * S)),
-                           dim3(kLdsThreads), lds, st, a);
+    const dim3 grid(static_cast<unsigned>(tiles * S));
+    if (twg && c2)
+        hipLaunchKernelGGL((ntt_eras_kernel<true, true>), grid, dim3(kLdsThreads), lds, st, a);
+    else if (twg)
+        hipLaunchKernelGGL((ntt_eras_kernel<true, false>), grid, dim3(kLdsThreads), lds, st, a);
+    else if (c2)
+        hipLaunchKernelGGL((ntt_eras_kernel<false, true>), grid, dim3(kLdsThreads), lds, st, a);
     else
-        hipLaunchKernelGGL(ntt_eras_kernel<false>, dim3(static_cast<unsigned>(tiles * S)),
-                           dim3(kLdsThreads), lds, st, a);
+        hipLaunchKernelGGL((ntt_eras_kernel<false, false>), grid, dim3(kLdsThreads), lds, st,
+                           a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1813,8 +1892,11 @@ std::string ntt_kernel_names(const qi_plan* p, bool decode)
     if (eras_plan(p) && (decode || p->sys)) {
         bool twg;
         (void)eras_geom(p, &twg);
-        return std::string(decode ? "eras_ctx_kernel + " : "") +
-               (twg ? "ntt_eras_kernel<true>" : "ntt_eras_kernel<false>");
+        XfPlan pl[4];
+        (void)eras_tw_words(p, pl);
+        const bool c2 = decode && !p->sys && eras_c2(pl[kTwPni], p->n - p->k, eras_geom(p, &twg));
+        return std::string(decode ? "eras_ctx_kernel + " : "") + "ntt_eras_kernel<" +
+               (twg ? "true" : "false") + ", " + (c2 ? "true" : "false") + ">";
     }
     if (!lds_engine(p))
         return decode ? "ntt_ctx_kernel + ntt_expand_kernel + ntt_fix_kernel + ntt_pass_kernel"

@@ -25,12 +25,12 @@ def kernels():
         pytest.skip("kernel resource report not built (make -C quadiron_amd/csrc)")
     out, cur = {}, None
     for line in (ln for r in RES for ln in open(r)):
-        m = re.search(r"remark: Function Name: (\S+)", line)
+        m = re.search(r"remark: (?:\S+:\d+:\d+: )?Function Name: (\S+)", line)
         if m:
             cur = m.group(1)
             out[cur] = {}
             continue
-        m = re.search(r"remark:\s+([A-Za-z ]+?)(?: \[[^\]]*\])?: (\d+)", line)
+        m = re.search(r"remark: (?:\S+:\d+:\d+: )?\s*([A-Za-z ]+?)(?: \[[^\]]*\])?: (\d+)", line)
         if m and cur:
             out[cur][m.group(1).strip()] = int(m.group(2))
     return out

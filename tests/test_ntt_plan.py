@@ -248,3 +248,26 @@ def test_erasure_decode_math(n, k, sys_):
     ninv = pow(n, Q - 2, Q)
     d = [sum(full[j] * pow(ri, j * t, Q) for j in range(n)) * ninv % Q for t in range(k)]
     assert d == P
+    # the kernel's two-pass completion (ntt_eras_kernel, INTT_n in two
+    # passes, n = R0 R1): the unit pass of the zero-filled codeword plus its
+    # response to c_E, then the last pass alone
+    lg = n.bit_length() - 1
+    lg0 = (lg + 1) // 2
+    R0, R1 = 1 << lg0, 1 << (lg - lg0)
+    w1i = pow(ri, R0, Q)  # w_R1^-1
+    # unit pass: group g (elements t = g + R0 q), output u
+    Y = [[sum(cz[g + R0 * q] * pow(w1i, q * u, Q) for q in range(R1)) % Q
+          for u in range(R1)] for g in range(R0)]
+    for a_, t in enumerate(E):
+        g, q0 = t % R0, t // R0
+        for u in range(R1):
+            Y[g][u] = (Y[g][u] + cE[a_] * pow(w1i, q0 * u, Q)) % Q
+    # last pass: task j < R1 over the groups v, input twiddle w_n^-jv, then an
+    # R0-point inverse DFT; output m is t = j + R1 m
+    w0i = pow(ri, R1, Q)  # w_R0^-1
+    out = [0] * n
+    for j in range(R1):
+        for m in range(R0):
+            out[j + R1 * m] = sum(Y[v][j] * pow(ri, j * v, Q) * pow(w0i, v * m, Q)
+                                  for v in range(R0)) % Q
+    assert [out[t] * ninv % Q for t in range(k)] == P

@@ -7,7 +7,7 @@ import sys
 from collections import Counter
 
 import os
-s = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'build', 'obj', 'kernels.s')).read()
+s = open(os.environ.get('QI_ASM', os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'build', 'obj', 'kernels.s'))).read()
 pats = sys.argv[1:] or ['encode_fnt_kernelILi16ELi2ELb1ELb1E', 'matrix_kernelILi8ELi4ELb1E']
 meta = {}
 for m in re.finditer(r'\.name:\s+(\S+)\n', s):

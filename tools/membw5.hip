@@ -27,7 +27,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 }
 // RPI rows per store instruction; RBO 0: wave w takes row blocks w + 4 j,
 // 1: row blocks 16 w + j; AUX store policy
-template <int RPI, int RBO, int AUX>
+template <int RPI, int RBO, int AUX, int ROT = 0>
 __global__ __launch_bounds__(256) void enc(const uint16_t* in, uint16_t* out, int tiles)
 {
     const int b = blockIdx.x;
@@ -52,7 +52,9 @@ __global__ __launch_bounds__(256) void enc(const uint16_t* in, uint16_t* out, in
     const int lr = l / LPR, lc = l % LPR;
     constexpr int NI = 8 / RPI;  // instructions per 16-row x 64 / ... group
 #pragma unroll 1
-    for (int jj = 0; jj < 16; jj++) {
+    for (int j0 = 0; j0 < 16; j0++) {
+        // ROT: the row-block walk starts at a per-stripe offset
+        const int jj = ROT ? (j0 + ROT * s) & 15 : j0;
         const int rb = RBO == 0 ? w + 4 * jj : 16 * w + jj;
         // 16 rows x 1 KB = 16 instructions of 1 KB
 #pragma unroll
@@ -109,23 +111,22 @@ int main(int argc, char** argv)
     CHECK(hipMemset(b, 2, bb));
     const double eb = ab + bb;
     const int tiles = P / TW;
-#define RUN(RPI, RBO, AUX)                                                                   \
+#define RUN(RPI, RBO, AUX, ROT)                                                                   \
     {                                                                                        \
-        float ms = timeit([&] { enc<RPI, RBO, AUX><<<tiles * S, 256, 80 * 1024>>>(a, b, tiles); }, \
+        float ms = timeit([&] { enc<RPI, RBO, AUX, ROT><<<tiles * S, 256, 80 * 1024>>>(a, b, tiles); }, \
                           reps);                                                             \
-        printf("cfg3enc RPI%d rbo%d aux%2d %7.3f ms %7.1f GB/s\n", RPI, RBO, AUX, ms,         \
+        printf("cfg3enc RPI%d rbo%d aux%2d rot%d %7.3f ms %7.1f GB/s\n", RPI, RBO, AUX, ROT, ms,         \
                eb / ms / 1e6);                                                               \
     }
     for (int rep = 0; rep < 2; rep++) {
         printf("--- rep %d\n", rep);
-        RUN(8, 0, 18)
-        RUN(8, 0, 0)
-        RUN(8, 1, 18)
-        RUN(4, 0, 18)
-        RUN(2, 0, 18)
-        RUN(1, 0, 18)
-        RUN(1, 0, 0)
-        RUN(1, 1, 18)
+        RUN(8, 0, 18, 0)
+        RUN(8, 0, 18, 1)
+        RUN(8, 0, 18, 5)
+        RUN(8, 0, 18, 7)
+        RUN(8, 0, 0, 0)
+        RUN(8, 0, 0, 5)
+        RUN(4, 0, 18, 5)
     }
     return 0;
 }
