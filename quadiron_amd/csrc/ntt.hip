@@ -396,7 +396,8 @@ __global__ __launch_bounds__(kNttBlock) void ntt_fix_kernel(NttFixArgs a)
 // LDS-resident engine (max(n, len_2k) <= kLdsMaxN): one workgroup runs every
 // transform of a tile of T columns of one stripe in LDS, so HBM sees only the
 // algorithmic bytes (the k input rows and the output rows).  The tile is an
-// nmax x T int32 image (element (position, column) at buf[pos T + col]);
+// nmax x T int32 image (element (position, column) at buf[prow(pos) T +
+// col]: an empty row after every 32, see prow);
 // radix <= 32 passes, with every lane on one column of one butterfly group:
 //   forward transforms: decimation in frequency (natural order in, output
 //     X[j] at position pos(j) -- a mixed-radix digit reversal);
@@ -440,6 +441,20 @@ __device__ __forceinline__ int xf_index(const XfPlan& P, int p)
         b += P.lgr[q];
     }
     return t;
+}
+
+// Image row of transform position p: one empty row after every 32.  A
+// wave holds 64 / T tasks of a pass; in the short-stride passes (the unit
+// pass: 32 consecutive positions per task) those tasks sat 32 T words
+// apart, i.e. on the same banks (k1000 encode: 72 % of the LDS cycles were
+// bank conflicts); one row per 32 moves task tt by tt T banks.  A pass
+// task's positions b + j + q s (b a multiple of 32 or the task inside one
+// aligned 32-block, j < s) never carry into bit 5, so
+// prow(b + j + q s) = prow(b + j) + prow(q s): a per-task base plus a
+// per-q uniform offset, as before.
+__host__ __device__ __forceinline__ int prow(int p)
+{
+    return p + (p >> 5);
 }
 
 enum : int { kLdsEnc = 0, kLdsSysEnc = 1, kLdsDec = 2, kLdsSysDec = 3 };
@@ -495,12 +510,12 @@ __device__ __forceinline__ void lds_pass_body(int32_t* buf, const int32_t* twp, 
         // transform bi of the batch (at image row bi N), its task tt
         const int bi = t2 >> lgtasks, tt = t2 & ((1 << lgtasks) - 1);
         const int j = UNIT ? 0 : tt & ((1 << lgs) - 1);
-        const int lb = ((bi * N + ((tt >> lgs) << lgL) + j) << lgT) + col;
+        const int lb = (prow(bi * N + ((tt >> lgs) << lgL) + j) << lgT) + col;
         const int32_t* tj = twp + j * R;
         int32_t v[R], w[R];
 #pragma unroll
         for (int q = 0; q < R; q++) {
-            v[q] = buf[lb + ((q << lgs) << lgT)];
+            v[q] = buf[lb + (prow(q << lgs) << lgT)];
             if (!UNIT)
                 w[q] = tj[q];
         }
@@ -522,7 +537,7 @@ __device__ __forceinline__ void lds_pass_body(int32_t* buf, const int32_t* twp, 
                 const int32_t c = cm[((ci0 + (u << cb)) << lgnb) + bi];
                 y = mul_rt(y, CANON ? balanced(static_cast<uint32_t>(c)) : c);
             }
-            buf[lb + ((u << lgs) << lgT)] = y;
+            buf[lb + (prow(u << lgs) << lgT)] = y;
         }
     }
 }
@@ -601,7 +616,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     extern __shared__ int32_t qi_ntt_lds[];
     const int nmax = a.nmax, lgT = a.lgT, T = 1 << lgT, k = a.k;
     int32_t* buf = qi_ntt_lds;
-    int32_t* tw_l = qi_ntt_lds + (nmax << lgT);  // pass twiddle tables
+    int32_t* tw_l = qi_ntt_lds + (prow(nmax) << lgT);  // pass twiddle tables
     const int32_t* tw = TWG ? a.tw : tw_l;
     int32_t* s_inv = TWG ? tw_l : tw_l + a.tw_words;  // inv_A_i (balanced)
     int32_t* s_id = s_inv + k;                 // received ids z_i
@@ -669,7 +684,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
         }
         lo = int4{e[0], e[1], e[2], e[3]};
         hi = int4{e[4], e[5], e[6], e[7]};
-        int4* d = reinterpret_cast<int4*>(buf + ((p) << lgT) + 8 * cj);
+        int4* d = reinterpret_cast<int4*>(buf + (prow(p) << lgT) + 8 * cj);
         d[0] = lo;
         d[1] = hi;
     };
@@ -705,7 +720,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
             for (int u = 0; u < kLdsBatch; u++) {
                 const int p = p0 + u * G;
                 if (p < a.n)
-                    buf[((p) << lgT) + col] = x[u];
+                    buf[(prow(p) << lgT) + col] = x[u];
             }
         }
         __syncthreads();
@@ -713,7 +728,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     } else {
         // INTT_n input (DIT order): zero, then y_i = v_i inv_A_i at pos_n(z_i)
         for (int p = g; p < a.n; p += G)
-            buf[((p) << lgT) + col] = 0;
+            buf[(prow(p) << lgT) + col] = 0;
         __syncthreads();
         if (a.wide) {
             for (int i0 = rl; i0 < k; i0 += RPP * kLdsBatch) {
@@ -745,7 +760,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
             for (int u = 0; u < kLdsBatch; u++) {
                 const int i = i0 + u * G;
                 if (i < k)
-                    buf[((xf_pos(a.pnf, s_id[i])) << lgT) + col] = mul_rt(x[u], s_inv[i]);
+                    buf[(prow(xf_pos(a.pnf, s_id[i])) << lgT) + col] = mul_rt(x[u], s_inv[i]);
             }
         }
         __syncthreads();
@@ -769,7 +784,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
                     const long long c = static_cast<long long>(
                                             a.in_oor.entries[bk * a.in_oor.cap + e]) - c0;
                     if (c >= 0 && c < T)
-                        buf[((p) << lgT) + static_cast<int>(c)] = y;
+                        buf[(prow(p) << lgT) + static_cast<int>(c)] = y;
                 }
             }
             __syncthreads();
@@ -783,9 +798,9 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
         const int h = a.len2k >> 1;
         const int32_t* twist = tw + a.twist;
         for (int t = g; t < h; t += G) {
-            const int32_t x = t < k ? buf[(t << lgT) + col] : 0;
-            buf[(t << lgT) + col] = x;
-            buf[((h + t) << lgT) + col] = t < k ? mul_rt(x, twist[t]) : 0;
+            const int32_t x = t < k ? buf[(prow(t) << lgT) + col] : 0;
+            buf[(prow(t) << lgT) + col] = x;
+            buf[(prow(h + t) << lgT) + col] = t < k ? mul_rt(x, twist[t]) : 0;
         }
         __syncthreads();
         // both NTT_h (DIF) at once, times C[2m + bi] in the last pass
@@ -795,15 +810,15 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
             lds_transform<true, false, false>(buf, tw, a.p2f, lgT, col, g, G, s_c, 1);
         lds_transform<false, true>(buf, tw, a.p2i, lgT, col, g, G, nullptr, 1);
         for (int t = g; t < k; t += G) {
-            const int32_t e = buf[(t << lgT) + col];
-            const int32_t o = mul_rt(buf[((h + t) << lgT) + col], twist[h + t]);
-            buf[(t << lgT) + col] = fold(e + o);  // [-65538, 131072] -> V range
+            const int32_t e = buf[(prow(t) << lgT) + col];
+            const int32_t o = mul_rt(buf[(prow(h + t) << lgT) + col], twist[h + t]);
+            buf[(prow(t) << lgT) + col] = fold(e + o);  // [-65538, 131072] -> V range
         }
         __syncthreads();
         if (a.mode != kLdsDec) {
             // systematic: evaluate the coefficients at r^t (NTT_n, DIF)
             for (int p = k + g; p < a.n; p += G)
-                buf[((p) << lgT) + col] = 0;
+                buf[(prow(p) << lgT) + col] = 0;
             __syncthreads();
             lds_transform<true, false>(buf, tw, a.pnf, lgT, col, g, G);
         }
@@ -817,7 +832,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
         for (int r = rl; r < a.out_rows; r += RPP) {
             const int t = a.out_first + r;
             const int p = natural ? t : xf_pos(a.pnf, t);
-            const int4* sp = reinterpret_cast<const int4*>(buf + ((p) << lgT) + 8 * cj);
+            const int4* sp = reinterpret_cast<const int4*>(buf + (prow(p) << lgT) + 8 * cj);
             const int4 lo = sp[0], hi = sp[1];
             const int32_t e[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
             uint32_t cv[8];
@@ -853,7 +868,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
     for (int r = g; r < a.out_rows; r += G) {
         const int t = a.out_first + r;
         const int p = natural ? t : xf_pos(a.pnf, t);
-        const uint32_t cv = canon_vr(buf[((p) << lgT) + col]);
+        const uint32_t cv = canon_vr(buf[(prow(p) << lgT) + col]);
         a.out[s * a.oss + r * a.ors + cg] = static_cast<uint16_t>(cv);
         if (cv == 65536u && a.out_oor.counts) {
             const long long bk = static_cast<long long>(s) * a.out_oor.slots + r;
@@ -910,12 +925,12 @@ __device__ void lds_intt_top(int32_t* buf, const int32_t* tw, const XfPlan& P, i
         const int umin = k > j ? (k - j + sN - 1) >> lgs : 0;
         if (umin >= R)
             continue;
-        const int lb = (j << lgT) + col;
+        const int lb = (prow(j) << lgT) + col;
         int32_t v[32];
 #pragma unroll
         for (int q = 0; q < 32; q++) {
             if (q < R) {
-                v[q] = buf[lb + ((q << lgs) << lgT)];
+                v[q] = buf[lb + (prow(q << lgs) << lgT)];
                 if (q > 0 && lgs > 0)
                     v[q] = mul_rt(v[q], twp[j * R + q]);
             }
@@ -931,7 +946,7 @@ __device__ void lds_intt_top(int32_t* buf, const int32_t* tw, const XfPlan& P, i
             if (syn)
                 syn[(((j + (u << lgs)) - k) << lgT) + col] = fold(fold(acc));
             else
-                buf[lb + ((u << lgs) << lgT)] = fold(fold(acc));
+                buf[lb + (prow(u << lgs) << lgT)] = fold(fold(acc));
         }
     }
     __syncthreads();
@@ -1064,11 +1079,11 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
     extern __shared__ int32_t qi_ntt_lds[];
     const int n = a.n, lgT = a.lgT, T = 1 << lgT, k = a.k, e = a.eras_e;
     int32_t* buf = qi_ntt_lds;
-    int32_t* tw_l = buf + (n << lgT);
+    int32_t* tw_l = buf + (prow(n) << lgT);
     const int32_t* tw = TWG ? a.tw : tw_l;
     int32_t* s_id = TWG ? tw_l : tw_l + a.tw_words;
-    int32_t* s_pos = s_id + k;
-    int32_t* s_eid = s_pos + n;
+    int32_t* s_pos = s_id + k;  // C2: e x T words of syndromes instead
+    int32_t* s_eid = s_pos + (C2 ? (e << lgT) : n);
     int32_t* s_B = s_eid + e;
     int32_t* s_cE = s_B + e * e;
     int32_t* s_rinv = s_cE + (e << lgT);  // w_R^-x of INTT_n's last pass
@@ -1089,8 +1104,9 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
             tw_l[i] = a.tw[i];
     for (int i = tid; i < k; i += kLdsThreads)
         s_id[i] = ctx[a.ids_off + i];
-    for (int t = tid; t < n; t += kLdsThreads)
-        s_pos[t] = ctx[a.pos_off + t];
+    if (!C2)
+        for (int t = tid; t < n; t += kLdsThreads)
+            s_pos[t] = ctx[a.pos_off + t];
     for (int j = tid; j < e; j += kLdsThreads)
         s_eid[j] = ctx[a.eras_eid + j];
     for (int i = tid; i < e * e; i += kLdsThreads)
@@ -1126,7 +1142,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
                     if (i < k) {
                         const uint32_t xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
                         int4* d = reinterpret_cast<int4*>(
-                            buf + (xf_pos(a.pni, s_id[i]) << lgT) + 8 * cj);
+                            buf + (prow(xf_pos(a.pni, s_id[i])) << lgT) + 8 * cj);
                         d[0] = int4{static_cast<int32_t>(xs[0] & 0xffffu),
                                     static_cast<int32_t>(xs[0] >> 16),
                                     static_cast<int32_t>(xs[1] & 0xffffu),
@@ -1150,13 +1166,13 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
                 for (int u = 0; u < kLdsBatch; u++) {
                     const int i = i0 + u * G;
                     if (i < k)
-                        buf[(xf_pos(a.pni, s_id[i]) << lgT) + col] = x[u];
+                        buf[(prow(xf_pos(a.pni, s_id[i])) << lgT) + col] = x[u];
                 }
             }
         }
         for (int it = tid; it < (e << lgT); it += kLdsThreads) {
             const int j = it >> lgT, c = it & (T - 1);
-            buf[(xf_pos(a.pni, s_eid[j]) << lgT) + c] = fill ? s_cE[it] : 0;
+            buf[(prow(xf_pos(a.pni, s_eid[j])) << lgT) + c] = fill ? s_cE[it] : 0;
         }
         __syncthreads();
         if (a.in_oor.counts) {
@@ -1176,7 +1192,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
                     const long long c = static_cast<long long>(
                                             a.in_oor.entries[bk * a.in_oor.cap + f]) - c0;
                     if (c >= 0 && c < T)
-                        buf[(p << lgT) + static_cast<int>(c)] = -1;
+                        buf[(prow(p) << lgT) + static_cast<int>(c)] = -1;
                 }
             }
             __syncthreads();
@@ -1191,7 +1207,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
         const int32_t* Bj = s_B + j * e;
         int32_t acc = 0;  // |acc| <= 64 * 65536
         for (int u = 0; u < e; u++)
-            acc += mul_rt(C2 ? s_syn[(u << lgT) + c] : buf[((k + u) << lgT) + c], Bj[u]);
+            acc += mul_rt(C2 ? s_syn[(u << lgT) + c] : buf[(prow(k + u) << lgT) + c], Bj[u]);
         s_cE[it] = fold(fold(acc));  // [-1, 65536]
     }
     __syncthreads();
@@ -1226,7 +1242,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
                 const int u = it >> lgT, c = it & (T - 1);
                 for (int j = 0; j < e; j++) {
                     const int t = s_eid[j], q0 = t >> lg0;
-                    int32_t* d = buf + ((((t & m0) << lg1) + u) << lgT) + c;
+                    int32_t* d = buf + (prow(((t & m0) << lg1) + u) << lgT) + c;
                     // w_R1^-x = w_R0^(-x R0 / R1)
                     const int32_t w = s_rinv[((q0 * u) << (lg0 - lg1)) & m0];
                     *d = fold(fold(*d + mul_rt(s_cE[(j << lgT) + c], w)));
@@ -1266,7 +1282,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
             if (!wvalid)
                 return;
             for (int r = rl; r < a.out_rows; r += RPP) {
-                const int4* sp = reinterpret_cast<const int4*>(buf + (r << lgT) + 8 * cj);
+                const int4* sp = reinterpret_cast<const int4*>(buf + (prow(r) << lgT) + 8 * cj);
                 const int4 lo = sp[0], hi = sp[1];
                 const int32_t v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
                 uint32_t cv[8];
@@ -1281,7 +1297,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
             return;
         for (int r = g; r < a.out_rows; r += G)
             a.out[s * a.oss + r * a.ors + cg] = static_cast<uint16_t>(
-                canon_vr(fold(mul_rt(buf[(r << lgT) + col], a.inv_n))));
+                canon_vr(fold(mul_rt(buf[(prow(r) << lgT) + col], a.inv_n))));
         return;
     }
     // systematic (decode: the data rows t < k; encode: the parities t >= k):
@@ -1526,7 +1542,7 @@ int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab, int* twi
 // runs NTT_n alone)
 size_t lds_bytes(const qi_plan* p, int lgT, int tw_words, bool twg, int rows)
 {
-    return ((static_cast<size_t>(rows) << lgT) +
+    return ((static_cast<size_t>(prow(rows)) << lgT) +
             lds_side_words(tw_words, p->k, p->len2k, twg)) *
            4;
 }
@@ -1574,11 +1590,12 @@ bool lds_engine(const qi_plan* p)
 }
 
 // ---- erasure decode (ntt_eras_kernel) ----
-// the two-pass completion (ntt_eras_kernel<., true>): INTT_n in two passes
-// and the syndromes (e x T) fit the position map's n words
-static bool eras_c2(const XfPlan& pni, int e, int lgT)
+// the two-pass completion (ntt_eras_kernel<., true>): the non-systematic
+// decode of a two-pass INTT_n; it reads no position map, and that region
+// holds the e x T syndromes instead
+static bool eras_c2(const XfPlan& pni)
 {
-    return pni.np == 2 && (static_cast<long long>(e) << lgT) <= pni.N;
+    return pni.np == 2;
 }
 
 bool eras_plan(const qi_plan* p)
@@ -1591,10 +1608,11 @@ ErasCtxLayout eras_layout(const qi_plan* p)
     return ErasCtxLayout{p->k, p->n, p->n - p->k};
 }
 
-size_t eras_bytes(const qi_plan* p, int lgT, int tw_words, bool twg)
+size_t eras_bytes(const qi_plan* p, int lgT, int tw_words, bool twg, bool c2)
 {
     const ErasCtxLayout L = eras_layout(p);
-    return ((static_cast<size_t>(p->n) << lgT) + (twg ? 0 : tw_words) + L.k + L.n + L.e +
+    const size_t posw = c2 ? static_cast<size_t>(L.e) << lgT : static_cast<size_t>(L.n);
+    return ((static_cast<size_t>(prow(p->n)) << lgT) + (twg ? 0 : tw_words) + L.k + posw + L.e +
             static_cast<size_t>(L.e) * L.e + (static_cast<size_t>(L.e) << lgT) + 32) *
            4;
 }
@@ -1606,18 +1624,25 @@ int eras_tw_words(const qi_plan* p, XfPlan* pl)
     return pl[kTwP2f].tw[0];
 }
 
-int eras_geom(const qi_plan* p, bool* twg)
+// tile width (log2 T) at two workgroups per CU, tables staged when they
+// fit; *c2: the launch takes the two-pass completion (dec: a non-systematic
+// decode)
+int eras_geom(const qi_plan* p, bool dec, bool* twg, bool* c2)
 {
     XfPlan pl[4];
     const int tw_words = eras_tw_words(p, pl);
     for (int g = 0; g < 2; g++)
-        for (int lg = 6; lg >= 3; lg--)
-            if (eras_bytes(p, lg, tw_words, g == 1) <= kLdsCap / 2) {
+        for (int lg = 6; lg >= 3; lg--) {
+            const bool two = dec && eras_c2(pl[kTwPni]);
+            if (eras_bytes(p, lg, tw_words, g == 1, two) <= kLdsCap / 2) {
                 *twg = g == 1;
+                *c2 = two;
                 return lg;
             }
+        }
     *twg = false;
-    return eras_bytes(p, 3, tw_words, false) <= kLdsCap ? 3 : -1;
+    *c2 = dec && eras_c2(pl[kTwPni]);
+    return eras_bytes(p, 3, tw_words, false, *c2) <= kLdsCap ? 3 : -1;
 }
 
 int eras_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
@@ -1633,8 +1658,8 @@ int eras_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
     int rinv_off = 0;
     lds_tables(p, pl, nullptr, nullptr, &rinv_off);
     a.rinv = p->d_ldstw ? p->d_ldstw + rinv_off : nullptr;
-    bool twg;
-    a.lgT = eras_geom(p, &twg);
+    bool twg, c2;
+    a.lgT = eras_geom(p, a.mode == kLdsDec, &twg, &c2);
     if (a.lgT < 0 || !a.tw)
         return -3;
     const ErasCtxLayout L = eras_layout(p);
@@ -1656,8 +1681,7 @@ int eras_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
                  (!r.base1 || (al(r.base1) && a8(r.ss1) && a8(r.rs1))) && al(a.out) &&
                  a8(a.oss) && a8(a.ors);
     }
-    const size_t lds = eras_bytes(p, a.lgT, a.tw_words, twg);
-    const bool c2 = a.mode == kLdsDec && eras_c2(a.pni, L.e, a.lgT);
+    const size_t lds = eras_bytes(p, a.lgT, a.tw_words, twg, c2);
     const void* fn =
         twg ? (c2 ? reinterpret_cast<const void*>(&ntt_eras_kernel<true, true>)
                   : reinterpret_cast<const void*>(&ntt_eras_kernel<true, false>))
@@ -1890,11 +1914,8 @@ int ntt_plan_init(qi_plan* p)
 std::string ntt_kernel_names(const qi_plan* p, bool decode)
 {
     if (eras_plan(p) && (decode || p->sys)) {
-        bool twg;
-        (void)eras_geom(p, &twg);
-        XfPlan pl[4];
-        (void)eras_tw_words(p, pl);
-        const bool c2 = decode && !p->sys && eras_c2(pl[kTwPni], p->n - p->k, eras_geom(p, &twg));
+        bool twg, c2;
+        (void)eras_geom(p, decode && !p->sys, &twg, &c2);
         return std::string(decode ? "eras_ctx_kernel + " : "") + "ntt_eras_kernel<" +
                (twg ? "true" : "false") + ", " + (c2 ? "true" : "false") + ">";
     }
