@@ -4,6 +4,8 @@
 // and the OOR route tables of decode_prepare (src/fec_base.h:1361-1404).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "gf65537.h"
 #include "matrix_pack.h"
 #include "qi_internal.h"
@@ -200,30 +202,40 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
 // the columns' 1 / A'(x_i), row-scaled when an entry breaks coef_ok (as
 // pack_row_grp: the row's scale search on its 32-lane group), summed into
 // kcorr / kmf, and written as the [a | 0], [0 | b], [b | a] operand tiles.
-template <int NT>
-__device__ void pack_tiles_direct(const uint32_t* Mt, int kp, const uint32_t* cinv,
-                                  const MatLayout& L, int32_t* mat)
+// 4-entry groups per row of a context matrix, at most
+constexpr int kPackNj = kMatMaxKin / 4;
+
+// One pass: row blocks rb0, rb0 + 1 (rows 16 rb0 .. 16 rb0 + 31); row t's
+// canonical entries i0 .. i0 + 3 from ent(t, i0, e).  stg: 32 rows of the
+// (aw, bw) words of each group (LDS).
+template <int NT, class Ent>
+__device__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, const MatLayout& L,
+                                int32_t* mat, uint32_t (*stg)[2 * kPackNj])
 {
     constexpr int LPR = 32, ROWS = NT / LPR;  // 32 rows (two row blocks) per pass
     constexpr int MM = (kMatMaxKin / 4 + LPR - 1) / LPR;
-    constexpr int NJ = kMatMaxKin / 4;  // 4-entry groups per row, at most
-    __shared__ uint32_t stg[ROWS][2 * NJ];  // per row: (aw, bw) of each group
+    static_assert(ROWS == 32, "two row blocks per pass");
     const int k = L.kin, KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
     const int tid = threadIdx.x, sub = tid % LPR, rl = tid / LPR;
     int32_t* mf = mat + L.mf();
-    for (int rb0 = 0; rb0 < RB; rb0 += ROWS / 16) {
+    {
         const int t = 16 * rb0 + rl;
         if (t < L.R) {
             uint32_t v[MM][4];
             uint32_t bad = 0;
 #pragma unroll
-            for (int m = 0; m < MM; m++)
+            for (int m = 0; m < MM; m++) {
+                const int i0 = 4 * (sub + m * LPR);
+                uint32_t e[4] = {0u, 0u, 0u, 0u};
+                if (i0 < k)
+                    ent(t, i0, e);
 #pragma unroll
                 for (int jb = 0; jb < 4; jb++) {
-                    const int i = 4 * (sub + m * LPR) + jb;
-                    v[m][jb] = i < k ? mulm(Mt[static_cast<size_t>(t) * kp + i], cinv[i]) : 0u;
+                    const int i = i0 + jb;
+                    v[m][jb] = i < k ? mulm(e[jb], cinv[i]) : 0u;
                     bad |= i < k && !coef_ok(balanced(v[m][jb]));
                 }
+            }
             bad = grp_or(bad, LPR);
             uint32_t sc = 1;
             while (bad) {  // rare; uniform in the group
@@ -297,11 +309,25 @@ __device__ void pack_tiles_direct(const uint32_t* Mt, int kp, const uint32_t* ci
                     mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
                 if (KS < 4 || half == 1)
                     mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
-                mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
+                if (KS < 2)  // [b | a]: the kernels rebuild it at KS >= 2
+                    mf[base + 256] = static_cast<int32_t>(half ? aw : bw);
             }
         }
         __syncthreads();
     }
+}
+
+template <int NT>
+__device__ void pack_tiles_direct(const uint32_t* Mt, int kp, const uint32_t* cinv,
+                                  const MatLayout& L, int32_t* mat, uint32_t (*stg)[2 * kPackNj])
+{
+    auto ent = [&](int t, int i0, uint32_t (&e)[4]) {
+#pragma unroll
+        for (int jb = 0; jb < 4; jb++)
+            e[jb] = i0 + jb < L.kin ? Mt[static_cast<size_t>(t) * kp + i0 + jb] : 0u;
+    };
+    for (int rb0 = 0; rb0 < L.RB(); rb0 += 2)
+        pack_tiles_pass<NT>(rb0, ent, cinv, L, mat, stg);
 }
 
 // LDS row pitch of the context kernel's k x k matrix: 4 x odd, >= k
@@ -436,11 +462,13 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         const int32_t xi = balanced(xs[tid]);
         const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
         int32_t q = 1, h = 1;  // A[k]; Q_i(x_i) so far
-        if (mode == 0)
+        // (the chunked BIG rows are written by a second division below)
+        const bool rows = mode == 0 && !(BIG && !dot2);
+        if (rows)
             Mt[(k - 1) * kp + tid] = 1;
         for (int j = k - 1; j >= 1; j--) {
             q = Ab[j] + mul_lz(q, xi);
-            if (mode == 0)
+            if (rows)
                 Mt[(j - 1) * kp + tid] = canon_lz(q);
             h = q + mul_lz(h, xi);
         }
@@ -482,15 +510,48 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         }
     }
     __syncthreads();
-    if (BIG && !dot2) {
-        // whole-tile widths: the operand tiles straight from the rows, two
-        // 16-row blocks at a time (32 lanes per row, 4 consecutive entries
-        // per lane and group: scale, split, staged in LDS, then stored
-        // rows-fastest as whole tile lines) -- no `plain` write-back, no
-        // re-read of the rows, no dot2 section (the kernels take single
-        // coefficients from the tiles)
-        pack_tiles_direct<NT>(Mt, kp, cinv, L, mat);
-        return;
+    if constexpr (BIG) {
+        __shared__ uint32_t stg[32][2 * kPackNj];
+        if (!dot2 && mode == 0) {
+            // whole-tile widths, non-systematic: the rows in 32-row chunks
+            // from the top, never in global memory.  Thread i runs Q_i's
+            // synthetic division again (1 / A'(x_i) is known now), writing
+            // the chunk's rows into LDS; then the chunk's two row blocks are
+            // packed straight into the operand tiles (32 lanes per row, 4
+            // entries per lane and group: scale, split, staged, stored
+            // rows-fastest as whole tile lines).  No `plain` rows, no dot2
+            // section (the kernels take single coefficients from the tiles).
+            uint32_t* ch = qi_ctx_lds;  // 32 x kpc
+            const int kpc = (k + 3) & ~3;
+            const int32_t xi = tid < k ? balanced(xs[tid]) : 0;
+            const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
+            int32_t q = 1;
+            for (int c = (k - 1) >> 5; c >= 0; c--) {
+                const int lo = 32 * c, hi = min(k, lo + 32);
+                if (tid < k) {
+                    for (int t = hi - 1; t >= lo; t--) {
+                        if (t < k - 1)
+                            q = Ab[t + 1] + mul_lz(q, xi);
+                        ch[(t - lo) * kpc + tid] = canon_lz(q);
+                    }
+                }
+                __syncthreads();
+                auto ent = [&](int t, int i0, uint32_t (&e)[4]) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(ch + (t - lo) * kpc + i0);
+                    e[0] = v.x;
+                    e[1] = v.y;
+                    e[2] = v.z;
+                    e[3] = v.w;
+                };
+                pack_tiles_pass<NT>(lo >> 4, ent, cinv, L, mat, stg);  // ends with a barrier
+            }
+            return;
+        }
+        if (!dot2) {
+            // systematic: the rows were built in `plain` (global) above
+            pack_tiles_direct<NT>(Mt, kp, cinv, L, mat, stg);
+            return;
+        }
     }
     {
         // LPR lanes per row: 4 entries per lane at k = 64
@@ -568,7 +629,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                         mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
                     if (KS < 4 || half == 1)
                         mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
-                    mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
+                    if (KS < 2)  // [b | a]: the kernels rebuild it at KS >= 2
+                    mf[base + 256] = static_cast<int32_t>(half ? aw : bw);
                 }
             }
         }
@@ -875,7 +937,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
                     mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
                 if (KS < 4 || half == 1)
                     mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
-                mf[base + 256] = static_cast<int32_t>(half ? aw : bw);      // [b | a]
+                if (KS < 2)  // [b | a]: the kernels rebuild it at KS >= 2
+                    mf[base + 256] = static_cast<int32_t>(half ? aw : bw);
             }
         }
     }
@@ -964,7 +1027,23 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
         // the matrix rows in the context itself (no LDS image); 1024 threads
         // keep 4x more of the packing and tile passes' row loads in flight
         // (k256 decode 0.81 -> 0.77 ms, k200 2.09 -> 2.05 ms)
-        hipLaunchKernelGGL((decode_ctx_kernel<1024, true>), dim3(S), dim3(1024), 0, st, k, r,
+        // (the non-systematic whole-tile contexts stage 32-row chunks of
+        // the matrix in the dynamic LDS)
+        const size_t lds = static_cast<size_t>(32) * ((k + 3) & ~3) * 4;
+        static std::atomic<uint64_t> attr_done{0};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess)
+            return -2;
+        const uint64_t bit = dev < 64 ? 1ull << dev : 0;
+        if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
+            if (hipFuncSetAttribute(
+                    reinterpret_cast<const void*>(&decode_ctx_kernel<1024, true>),
+                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                    static_cast<int>(32 * kMatMaxKin * 4)) != hipSuccess)
+                return -2;
+            attr_done.fetch_or(bit, std::memory_order_release);
+        }
+        hipLaunchKernelGGL((decode_ctx_kernel<1024, true>), dim3(S), dim3(1024), lds, st, k, r,
                            mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
                            slot_base, by_pos, words, dot2, err);
         return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -1169,12 +1169,22 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     const int32_t* rscale = M + L.rscale_mf();
     const int32_t* __restrict__ rowmap = a.rowmap;
     auto load_ops = [&](int rb, qi_v2i (&b)[KS][3], int32_t& kt, int32_t& rs, int32_t (&pr)[3]) {
+        // [b | a] is [0 | b] of the l' half over the h' K-steps and [a | 0]
+        // of the h' half over the l' K-steps, lane for lane (the same K
+        // offset within the half): from those registers at KS >= 2 (the
+        // contexts do not store it); at KS = 1 the halves share a K-step
+        // and sit in other lanes, so it is loaded
 #pragma unroll
         for (int ks = 0; ks < KS; ks++)
 #pragma unroll
-            for (int ty = 0; ty < 3; ty++)
+            for (int ty = 0; ty < (KS >= 2 ? 2 : 3); ty++)
                 b[ks][ty] = *reinterpret_cast<const qi_v2i*>(
                     mf + ((rb * KS + ks) * 3 + ty) * 128 + l * 2);
+        if constexpr (KS >= 2) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++)
+                b[ks][2] = ks < KS / 2 ? b[ks + KS / 2][1] : b[ks - KS / 2][0];
+        }
         // unconditional loads (a clamped row), selected after: an exec-masked
         // load leaves the compiler unsure how many vector-memory ops are in
         // flight, and it then drains vmcnt further than needed
@@ -1691,11 +1701,13 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
 
     // this wave's row blocks and their operand tiles, for the block's whole
-    // life: [a|0] over the h' K-steps, [0|b] over the l' K-steps, [b|a] over
-    // all (x64 pairs)
+    // life: [a|0] over the h' K-steps, [0|b] over the l' K-steps (x64
+    // pairs); [b|a] over the h' half is b1 and over the l' half b0, lane for
+    // lane (see matrix_mfma_kernel's load_ops), so it is neither stored in
+    // the context nor held twice
     int rbj[RPW];
     bool act[RPW];
-    qi_v4i b0[RPW][KS / 4], b1[RPW][KS / 4], b2[RPW][KS / 2];
+    qi_v4i b0[RPW][KS / 4], b1[RPW][KS / 4];
     int32_t kt[RPW], rs[RPW], pr[RPW][3];
 #pragma unroll
     for (int j = 0; j < RPW; j++) {
@@ -1712,11 +1724,6 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             b0[j][i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
             const qi_v2i y0 = ld2(KS / 2 + 2 * i, 1), y1 = ld2(KS / 2 + 2 * i + 1, 1);
             b1[j][i] = qi_v4i{y0.x, y0.y, y1.x, y1.y};
-        }
-#pragma unroll
-        for (int i = 0; i < KS / 2; i++) {
-            const qi_v2i x0 = ld2(2 * i, 2), x1 = ld2(2 * i + 1, 2);
-            b2[j][i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
         }
         const int t = 16 * rbc + tl;
         const int tcl = t < L.R ? t : L.R - 1;
@@ -1871,7 +1878,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
                         acc[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b1[j][i],
                                                                           acc[T][1], 0, 0, 0);
                     acc[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                        av[i], b2[j][hf * (KS / 4) + i], acc[T][2], 0, 0, 0);
+                        av[i], hf == 0 ? b1[j][i] : b0[j][i], acc[T][2], 0, 0, 0);
                 }
             }
         }
@@ -1897,7 +1904,11 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             // the coefficient from the wave's own operand tiles (no memory
             // load: waiting for one drained the stores and the prefetch)
             const int32_t corr = coef_from_tiles<KS>(
-                [&](int idx) { return pick_v4(b2[j], idx); }, pos, l);
+                [&](int idx) {
+                    // [b | a]'s dword idx: b1 over the h' pairs, b0 over the l'
+                    return idx < KS ? pick_v4(b1[j], idx) : pick_v4(b0[j], idx - KS);
+                },
+                pos, l);
 #pragma unroll
             for (int c = 0; c < 16; c++) {
                 const int32_t yc = fold(fold(y[c] - corr));

@@ -182,12 +182,13 @@ QI_HD int32_t pack_mf_dword(const MatLayout& L, const int32_t* rows, size_t d)
     return static_cast<int32_t>(v);
 }
 
-// Entry (t, i) of the row-scaled matrix read back from its [b | a] operand
-// tile (pack_mf_dword's layout: b at K = i, a at K = KH + i): 256 a + b,
-// canonical.  The decode paths that need single coefficients (the OOR
-// restore of the redo kernel, the dot2 sections filled on demand) take them
-// from here, so a context built for whole-tile widths holds the matrix only
-// once, as tiles.
+// Entry (t, i) of the row-scaled matrix read back from its operand tiles
+// (pack_mf_dword's layout): a from [a | 0] at K = i, b from [0 | b] at
+// K = KH + i; 256 a + b, canonical.  The decode paths that need single
+// coefficients (the OOR restore of the redo kernel, the dot2 sections
+// filled on demand) take them from here, so a context built for whole-tile
+// widths holds the matrix only once, as tiles -- and at KS >= 2 without
+// its [b | a] tiles, which repeat those two (the kernels rebuild them).
 QI_HD uint32_t mf_entry(const MatLayout& L, const int32_t* mf, int t, int i)
 {
     const int KS = L.KS(), KH = 16 * KS;
@@ -195,11 +196,11 @@ QI_HD uint32_t mf_entry(const MatLayout& L, const int32_t* mf, int t, int i)
     for (int h = 0; h < 2; h++) {
         const int K = h ? KH + i : i;
         const int ks = K >> 5, g = (K & 31) >> 3, dw = (K >> 2) & 1, jb = K & 3;
-        const size_t d = (static_cast<size_t>((t >> 4) * KS + ks) * 3 + 2) * 128 +
+        const size_t d = (static_cast<size_t>((t >> 4) * KS + ks) * 3 + h) * 128 +
                          static_cast<size_t>((16 * g + (t & 15)) * 2 + dw);
         e[h] = static_cast<int8_t>(static_cast<uint32_t>(mf[d]) >> (8 * jb));
     }
-    const int32_t c = 256 * e[1] + e[0];
+    const int32_t c = 256 * e[0] + e[1];
     return static_cast<uint32_t>(c < 0 ? c + kQ : c);
 }
 

@@ -190,6 +190,24 @@ static void test_matrix_mfma(std::mt19937_64& g)
                 return static_cast<int>(static_cast<int8_t>(
                     static_cast<uint32_t>(blk[dw]) >> (8 * (j % 4))));
             };
+            // the kernels rebuild [b | a] from the other two tiles at KS >= 2
+            // (the contexts do not store it) and read single entries back
+            // with mf_entry: both facts, for every dword and entry
+            if (KS >= 2)
+                for (int rb = 0; rb < L.RB(); rb++)
+                    for (int ks = 0; ks < KS; ks++)
+                        for (int lane = 0; lane < 64; lane++)
+                            for (int j = 0; j < 8; j++) {
+                                const int ba = opb(rb, ks, 2, lane, j);
+                                const int from = ks < KS / 2 ? opb(rb, ks + KS / 2, 1, lane, j)
+                                                             : opb(rb, ks - KS / 2, 0, lane, j);
+                                CHECK(ba == from, "[b|a] kin=%d ks=%d lane=%d", kin, ks, lane);
+                            }
+            for (int t = 0; t < R; t++)
+                for (int i = 0; i < kin; i++)
+                    CHECK(mf_entry(L, blk.data() + L.mf(), t, i) ==
+                              static_cast<uint32_t>(blk[L.plain() + static_cast<size_t>(t) * kin + i]),
+                          "mf_entry kin=%d t=%d i=%d", kin, t, i);
             for (int trial = 0; trial < 30; trial++) {
                 std::vector<uint32_t> x(kin);
                 for (auto& v : x)
