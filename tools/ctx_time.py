@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Time decode_ctx alone (cfg3 and cfg2 shapes) with HIP events; the library
-comes from QI_LIB_PATH (A/B of context-kernel variants)."""
+"""Time decode_ctx alone with HIP events; the library comes from QI_LIB_PATH
+(A/B of context-kernel variants).  Shapes k,m,S,P from the arguments
+(default: cfg3 and cfg2):  python tools/ctx_time.py 256,768,256,2048"""
 import os
 import sys
 import numpy as np
@@ -9,7 +10,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import quadiron_amd as qa
 
 torch.cuda.set_device(0)
-for k, m, S, P in ((64, 960, 1024, 2048), (16, 48, 4096, 32768)):
+shapes = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]] or \
+    [(64, 960, 1024, 2048), (16, 48, 4096, 32768)]
+for k, m, S, P in shapes:
     plan = qa.Plan(k, m, False)
     rng = np.random.default_rng(1)
     ids = np.stack([np.sort(rng.choice(k + m, k, replace=False)) for _ in range(S)])
