@@ -407,7 +407,48 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // ds_bpermute shifts and canonical mulm of round 2 took ~620 cycles per
     // step: 62 us of a k = 200 context).  A is monic: A[k] = 1 is set
     // explicitly, so k = 64 u needs no extra slot.  Stored balanced.
-    if (tid < 64) {  // wave 0 (wave-uniform)
+    if constexpr (BIG) {
+        // k > 128: A(x) by a product tree instead of k dependent steps on one
+        // wave (k = 256: 256 steps x 4 coefficient slots of DPP shifts and
+        // products).  Level l holds NL >> l polynomials of degree <= 2^l
+        // (2^l + 1 balanced coefficients each); leaf i is x - x_i, or 1 past
+        // k.  One thread per output coefficient of a level: its <= 2^l + 1
+        // lazy products (|sum| < 2^25), folded and stored balanced.  The
+        // critical path is ~NL products and log2 NL barriers.
+        __shared__ int32_t pt[2][2 * 512 + 4];
+        int NL = 1, lgl = 0;
+        while (NL < k) {
+            NL <<= 1;
+            lgl++;
+        }
+        for (int i = tid; i < NL; i += NT) {
+            pt[0][2 * i] = i < k ? -balanced(xs[i]) : 1;
+            pt[0][2 * i + 1] = i < k ? 1 : 0;
+        }
+        __syncthreads();
+        int cur = 0;
+        for (int lv = 0; lv < lgl; lv++) {
+            const int D = (1 << lv) + 1, D2 = (2 << lv) + 1, np = NL >> (lv + 1);
+            const int32_t* in = pt[cur];
+            int32_t* out = pt[cur ^ 1];
+            for (int it = tid; it < np * D2; it += NT) {
+                const int pp = it / D2, m = it - pp * D2;
+                const int32_t* Lp = in + (2 * pp) * D;
+                const int32_t* Rp = Lp + D;
+                const int a0 = m - (D - 1) > 0 ? m - (D - 1) : 0, a1 = m < D - 1 ? m : D - 1;
+                int32_t acc = 0;
+                for (int a = a0; a <= a1; a++)
+                    acc += mul_lz(Lp[a], Rp[m - a]);
+                out[pp * D2 + m] = balanced(canon_lz(fold(acc)));
+            }
+            __syncthreads();
+            cur ^= 1;
+        }
+        for (int i = tid; i < k; i += NT)
+            A[i] = static_cast<uint32_t>(pt[cur][i]);
+        if (tid == 0)
+            A[k] = 1;
+    } else if (tid < 64) {  // wave 0 (wave-uniform)
         constexpr int NS = kMatMaxKin / 64;
         const int nslot = (k + 63) / 64;
         int32_t xv[NS], au[NS];
