@@ -204,17 +204,25 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
 // kcorr / kmf, and written as the [a | 0], [0 | b], [b | a] operand tiles.
 // 4-entry groups per row of a context matrix, at most
 constexpr int kPackNj = kMatMaxKin / 4;
+// rows per chunk of the non-systematic k > 128 contexts (decode_ctx_kernel):
+// 64 rows = 4 row blocks per packing pass at 16 lanes per row (32 rows at 32
+// lanes: twice the passes and barriers for the same work; contexts k256
+// 120 -> 114 us, k300 179 -> 161 us, k384 219 -> 206 us)
+#ifndef QI_CTX_CHUNK
+#define QI_CTX_CHUNK 64
+#endif
+constexpr int kCtxChunk = QI_CTX_CHUNK;
 
-// One pass: row blocks rb0, rb0 + 1 (rows 16 rb0 .. 16 rb0 + 31); row t's
-// canonical entries i0 .. i0 + 3 from ent(t, i0, e).  stg: 32 rows of the
-// (aw, bw) words of each group (LDS).
-template <int NT, class Ent>
+// One pass: NT / LPR rows from row block rb0 on (LPR lanes per row); row
+// t's canonical entries i0 .. i0 + 3 from ent(t, i0, e).  stg: a row per
+// pass row of the (aw, bw) words of each group (LDS).
+template <int NT, int LPR, class Ent>
 __device__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, const MatLayout& L,
                                 int32_t* mat, uint32_t (*stg)[2 * kPackNj])
 {
-    constexpr int LPR = 32, ROWS = NT / LPR;  // 32 rows (two row blocks) per pass
+    constexpr int ROWS = NT / LPR;
     constexpr int MM = (kMatMaxKin / 4 + LPR - 1) / LPR;
-    static_assert(ROWS == 32, "two row blocks per pass");
+    static_assert(ROWS % 16 == 0, "whole row blocks per pass");
     const int k = L.kin, KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
     const int tid = threadIdx.x, sub = tid % LPR, rl = tid / LPR;
     int32_t* mf = mat + L.mf();
@@ -327,7 +335,7 @@ __device__ void pack_tiles_direct(const uint32_t* Mt, int kp, const uint32_t* ci
             e[jb] = i0 + jb < L.kin ? Mt[static_cast<size_t>(t) * kp + i0 + jb] : 0u;
     };
     for (int rb0 = 0; rb0 < L.RB(); rb0 += 2)
-        pack_tiles_pass<NT>(rb0, ent, cinv, L, mat, stg);
+        pack_tiles_pass<NT, 32>(rb0, ent, cinv, L, mat, stg);
 }
 
 // LDS row pitch of the context kernel's k x k matrix: 4 x odd, >= k
@@ -552,7 +560,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     }
     __syncthreads();
     if constexpr (BIG) {
-        __shared__ uint32_t stg[32][2 * kPackNj];
+        __shared__ uint32_t stg[kCtxChunk][2 * kPackNj];
         if (!dot2 && mode == 0) {
             // whole-tile widths, non-systematic: the rows in 32-row chunks
             // from the top, never in global memory.  Thread i runs Q_i's
@@ -562,13 +570,13 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             // entries per lane and group: scale, split, staged, stored
             // rows-fastest as whole tile lines).  No `plain` rows, no dot2
             // section (the kernels take single coefficients from the tiles).
-            uint32_t* ch = qi_ctx_lds;  // 32 x kpc
+            uint32_t* ch = qi_ctx_lds;  // kCtxChunk x kpc
             const int kpc = (k + 3) & ~3;
             const int32_t xi = tid < k ? balanced(xs[tid]) : 0;
             const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
             int32_t q = 1;
-            for (int c = (k - 1) >> 5; c >= 0; c--) {
-                const int lo = 32 * c, hi = min(k, lo + 32);
+            for (int c = (k - 1) / kCtxChunk; c >= 0; c--) {
+                const int lo = kCtxChunk * c, hi = min(k, lo + kCtxChunk);
                 if (tid < k) {
                     for (int t = hi - 1; t >= lo; t--) {
                         if (t < k - 1)
@@ -584,7 +592,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                     e[2] = v.z;
                     e[3] = v.w;
                 };
-                pack_tiles_pass<NT>(lo >> 4, ent, cinv, L, mat, stg);  // ends with a barrier
+                // (ends with a barrier)
+                pack_tiles_pass<NT, NT / kCtxChunk>(lo >> 4, ent, cinv, L, mat, stg);
             }
             return;
         }
@@ -1070,7 +1079,7 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
         // (k256 decode 0.81 -> 0.77 ms, k200 2.09 -> 2.05 ms)
         // (the non-systematic whole-tile contexts stage 32-row chunks of
         // the matrix in the dynamic LDS)
-        const size_t lds = static_cast<size_t>(32) * ((k + 3) & ~3) * 4;
+        const size_t lds = static_cast<size_t>(kCtxChunk) * ((k + 3) & ~3) * 4;
         static std::atomic<uint64_t> attr_done{0};
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess)
@@ -1080,7 +1089,7 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
             if (hipFuncSetAttribute(
                     reinterpret_cast<const void*>(&decode_ctx_kernel<1024, true>),
                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                    static_cast<int>(32 * kMatMaxKin * 4)) != hipSuccess)
+                    static_cast<int>(kCtxChunk * kMatMaxKin * 4)) != hipSuccess)
                 return -2;
             attr_done.fetch_or(bit, std::memory_order_release);
         }
