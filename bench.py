@@ -98,12 +98,20 @@ def _ref_leg(lib, k, m, P, threads, seconds, systematic, missing):
     import ctypes as C
     enc_b, dec_b = alg_bytes(k, m, P, systematic)
     stripes = C.c_longlong()
+    enc_s, dec_s = C.c_double(), C.c_double()
     wall = lib.ref_bench(int(systematic), k, m, C.c_size_t(P), C.c_double(seconds),
                          threads, missing.ctypes.data_as(C.c_void_p),
-                         C.byref(stripes), None, None)
+                         C.byref(stripes), C.byref(enc_s), C.byref(dec_s))
     n = stripes.value
+    # thread-time per stripe in each phase (the decode's share includes
+    # building its DecodeContext, src/fec_base.h:1177-1321)
+    enc_ms, dec_ms = enc_s.value / n * 1e3, dec_s.value / n * 1e3
     return {"value": n * (enc_b + dec_b) / wall / 1e9, "unit": "GB/s",
-            "cores": threads, "stripes": n, "wall_s": round(wall, 3)}
+            "cores": threads, "stripes": n, "wall_s": round(wall, 3),
+            "encode_ms_per_stripe": round(enc_ms, 4),
+            "decode_ms_per_stripe": round(dec_ms, 4),
+            "encode_GBps_per_thread": round(enc_b / enc_ms / 1e6, 3),
+            "decode_GBps_per_thread": round(dec_b / dec_ms / 1e6, 3)}
 
 
 def _port_leg(k, m, P, seconds, systematic, missing):
@@ -114,16 +122,21 @@ def _port_leg(k, m, P, seconds, systematic, missing):
     enc_b, dec_b = alg_bytes(k, m, P, systematic)
     rng = np.random.default_rng(1)
     data = rng.integers(0, 256, (k, 2 * P), dtype=np.uint8)
-    n, t0 = 0, time.perf_counter()
+    n, te, td, t0 = 0, 0.0, 0.0, time.perf_counter()
     while True:
+        a = time.perf_counter()
         outs, oor, cnt = oracle_encode_blocks(k, m, systematic, data)
+        b = time.perf_counter()
         oracle_decode_blocks(k, m, systematic, outs, oor, cnt, missing, data)
-        n += 1
-        wall = time.perf_counter() - t0
+        c = time.perf_counter()
+        te, td, n = te + b - a, td + c - b, n + 1
+        wall = c - t0
         if wall >= seconds:
             break
     return {"value": n * (enc_b + dec_b) / wall / 1e9, "unit": "GB/s",
-            "cores": 1, "stripes": n, "wall_s": round(wall, 3)}
+            "cores": 1, "stripes": n, "wall_s": round(wall, 3),
+            "encode_ms_per_stripe": round(te / n * 1e3, 4),
+            "decode_ms_per_stripe": round(td / n * 1e3, 4)}
 
 
 def cpu_baseline(k, m, P, systematic=False, seconds=1.0, threads=None):
@@ -163,7 +176,9 @@ def cpu_baseline(k, m, P, systematic=False, seconds=1.0, threads=None):
                       f"fixed n-k erasure pattern, >= {seconds:g} s per leg: "
                       f"{allc['stripes']} stripes on {allc['cores']} threads "
                       f"in {allc['wall_s']} s, {one['stripes']} stripes on 1 "
-                      f"thread in {one['wall_s']} s ({what})",
+                      f"thread in {one['wall_s']} s ({what}); per stripe on "
+                      f"1 thread: encode {one['encode_ms_per_stripe']} ms, "
+                      f"decode (context + apply) {one['decode_ms_per_stripe']} ms",
             "all_cores": allc, "one_core": one,
             "cpu": cpu_model(), "host_cpus": os.cpu_count()}
 
@@ -245,6 +260,8 @@ def parse_args(argv=None):
     ap.add_argument("--chunks", type=int, default=1)
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the cfg3 line the default (cfg2) run appends")
     ap.add_argument("--cpu-seconds", type=float, default=1.0)
     ap.add_argument("--dry-run", action="store_true",
                     help="launch/shard/reduce/report on the CPU (gloo), no "
@@ -291,24 +308,63 @@ def main(argv=None):
             torch.cuda.set_device(0)
         dev = torch.device("cuda", torch.cuda.current_device())
 
-    k, m, pkt_bytes, S = CONFIGS[args.cfg]
-    if args.stripes:
-        S = args.stripes
+    res = run_config(args.cfg, args.stripes, bool(args.systematic), args.steps,
+                     args.warmup, NC=max(1, args.chunks), n_streams=args.streams,
+                     dist=dist, dev=dev, dry=dry, rank=rank, world=world)
+    out = report(res, args.cfg, world, args.steps, args.warmup, dry)
+    ok = res["ok"]
+    # BASELINE.json configs[2] (k=64 n=1024 pkt=4KiB, 1024 stripes) in the
+    # same process, after the headline's timed region and in a timed region
+    # of its own: a driver-observed line for the high-fragmentation code
+    if (args.cfg == "cfg2" and not args.systematic and not args.no_secondary
+            and args.chunks == 1):
+        r3 = run_config("cfg3", None, False, max(5, min(args.steps, 20)), 3,
+                        dist=dist, dev=dev, dry=dry, rank=rank, world=world)
+        o3 = report(r3, "cfg3", world, r3["steps"], 3, dry)
+        out["secondary"] = {"cfg3": {
+            key: o3[key] for key in (
+                "metric", "value", "ms_per_step", "steps", "warmup", "config",
+                "hbm_fraction", "encode_kernel_ms", "encode_GBps", "decode_ms",
+                "decode_ctx_ms", "decode_GBps", "roundtrip_ok", "roofline",
+                "decode_roofline")}}
+        ok = ok and r3["ok"]
+    # the CPU baseline runs on rank 0 after the timed regions and their final
+    # barriers (every rank's kernels are done), at every world size, so a
+    # multi-GPU line carries the same-run CPU number as the 1-GPU one
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(res["k"], res["m"], res["P"],
+                                           res["sys"], args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()  # the other ranks wait for rank 0's CPU baseline
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
+               dev=None, dry=False, rank=0, world=1):
+    """Build one configuration's synthetic batch in HBM, run `warmup`
+    untimed steps, check the round trip, then time exactly `steps` steps
+    between barriers + device synchronisations (max over ranks).  One step =
+    encode every stripe (OOR recorded) + build the per-stripe decode
+    contexts (a random n-k erasure pattern per stripe) + decode every
+    stripe back to its k data rows."""
+    k, m, pkt_bytes, S = CONFIGS[cfg]
+    if stripes:
+        S = stripes
     P = pkt_bytes // 2
-    sys_ = bool(args.systematic)
-    headline = args.cfg == "cfg2" and not sys_
     n = 1
     while n < k + m:
         n *= 2
     lo, _ = shard(rank, world, S)
-    NC = max(1, args.chunks)
     assert S % NC == 0, "stripes must divide into chunks"
     C = S // NC
     ev = []
 
     if dry:
         # the same loop structure on a small CPU stand-in per step
-        n_out = n
         data = torch.zeros((NC, 1024), dtype=torch.int64)
         data += lo
 
@@ -319,6 +375,7 @@ def main(argv=None):
         def check():
             return True
         streams = [None]
+        plan = None
     else:
         plan = qa.Plan(k, m, sys_)
         n_out = plan.n_outputs
@@ -340,7 +397,7 @@ def main(argv=None):
         # another's decode (read-heavy); every slice is still encoded,
         # erased and decoded inside the timed step
         streams = ([torch.cuda.current_stream()] if NC == 1 else
-                   [torch.cuda.Stream() for _ in range(max(1, args.streams))])
+                   [torch.cuda.Stream() for _ in range(max(1, n_streams))])
         cstride = plan.ctx_bytes(1, P)
 
         def step(timed):
@@ -382,7 +439,7 @@ def main(argv=None):
         if not dry:
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step(False)
     sync()
     ok = check()  # the measured pipeline, outside the timed region
@@ -390,7 +447,7 @@ def main(argv=None):
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step(True)
     sync()
     if dist:
@@ -400,14 +457,53 @@ def main(argv=None):
     ok = ok and check()
     if dist:
         elapsed, ok = reduce_over_ranks(dist, elapsed, ok, dev)
-
-    enc_b, dec_b = alg_bytes(k, m, P, sys_)
-    value = aggregate_value(world, S, args.steps, k, m, P, elapsed, sys_)
-    enc_ms = dec_ms = ctx_ms = enc_gbs = dec_gbs = None  # dry run: no kernels
+    enc_ms = dec_ms = ctx_ms = None  # dry run: no kernels
     if ev:
         enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _, _ in ev]))
         ctx_ms = float(np.mean([b.elapsed_time(c) for _, b, c, _ in ev]))
         dec_ms = float(np.mean([b.elapsed_time(d) for _, b, _, d in ev]))
+    # the kernels this plan launches (the library's own dispatch,
+    # qi_gpu_kernels); the dry run names the cfg2 kernels it stands in for
+    if dry:
+        kernels = "encode=encode_fnt_kernel<16,2>; decode=(dry run: none)"
+    else:
+        kernels = plan.kernels(P)
+    return {"k": k, "m": m, "n": n, "P": P, "pkt_bytes": pkt_bytes, "S": S,
+            "C": C, "NC": NC, "sys": sys_, "steps": steps, "elapsed": elapsed,
+            "ok": ok, "enc_ms": enc_ms, "dec_ms": dec_ms, "ctx_ms": ctx_ms,
+            "kernels": kernels, "streams": len(streams)}
+
+
+def rocprof_record(key):
+    """profiles/rocprof_index.json entry for a bench configuration: the
+    rocprofv3 --stats average durations of its encode and decode kernels
+    (tools/rocprof_index.py, from the tracked *_kernel_stats.csv), with the
+    build they were measured on."""
+    path = os.path.join(ROOT, "profiles", "rocprof_index.json")
+    try:
+        with open(path) as f:
+            idx = json.load(f)
+    except (OSError, ValueError):
+        return None
+    rec = (idx.get("configs") or {}).get(key)
+    if not rec:
+        return None
+    rec = dict(rec)
+    rec.setdefault("build", idx.get("build"))
+    return rec
+
+
+def report(res, cfg, world, steps, warmup, dry):
+    """The bench line of one run_config result."""
+    k, m, n, P, S, C = (res[x] for x in ("k", "m", "n", "P", "S", "C"))
+    sys_, pkt_bytes = res["sys"], res["pkt_bytes"]
+    headline = cfg == "cfg2" and not sys_
+    enc_b, dec_b = alg_bytes(k, m, P, sys_)
+    elapsed = res["elapsed"]
+    value = aggregate_value(world, S, steps, k, m, P, elapsed, sys_)
+    enc_ms, dec_ms, ctx_ms = res["enc_ms"], res["dec_ms"], res["ctx_ms"]
+    enc_gbs = dec_gbs = None
+    if enc_ms:
         # per launch: C stripes (the whole batch unless chunked)
         enc_gbs = C * enc_b / (enc_ms * 1e-3) / 1e9
         dec_gbs = C * dec_b / (dec_ms * 1e-3) / 1e9
@@ -416,29 +512,42 @@ def main(argv=None):
     # rocprofv3 --pmc passes over a bench run of the same shape, FETCH_SIZE
     # doubled per MI355X_MICROARCH.md's gfx950 HBM note): HBM bytes and
     # VALU issue per launch of the encode kernel and of the decode kernels
-    pmc = pmc_record(args.cfg + ("_sys" if sys_ else ""), S)
+    key = cfg + ("_sys" if sys_ else "")
+    pmc = pmc_record(key, S)
+    # rocprofv3 average durations of the same kernels (tracked profiles),
+    # for a frac beside the event-timed one
+    rp = rocprof_record(key) if not dry else None
+    if rp and rp.get("stripes") != C:
+        rp = None
+    build = None if dry else qa.build_id()
     name = (f"RS-FNT{'-sys' if sys_ else ''} k={k} n={n} "
             f"pkt={pkt_bytes // 1024}KiB")
     metric = ("device-resident encode+decode GB/s per GPU, RS-FNT k=16 n=64 "
               "pkt=64KiB" if headline else
               f"device-resident encode+decode GB/s per GPU, {name}")
-    # the kernels this plan launches (the library's own dispatch,
-    # qi_gpu_kernels); the dry run names the cfg2 kernels it stands in for
-    if dry:
-        kernels = "encode=encode_fnt_kernel<16,2>; decode=(dry run: none)"
-    else:
-        kernels = plan.kernels(P)
-    enc_kernel, dec_kernels = (x.split("=", 1)[1] for x in kernels.split("; "))
+    enc_kernel, dec_kernels = (x.split("=", 1)[1]
+                               for x in res["kernels"].split("; "))
     penc = (pmc or {}).get("encode") or {}
     pdec = (pmc or {}).get("decode") or {}
+
+    def rocprof_frac(role, nbytes):
+        r = (rp or {}).get(role)
+        if not r or not r.get("avg_ms"):
+            return {}
+        same = bool(build and rp.get("build") and
+                    build.split("+src:")[-1] == rp["build"].split("+src:")[-1])
+        return {"frac_rocprof": nbytes / (r["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "rocprof_ms": r["avg_ms"], "rocprof_source": rp.get("source"),
+                "rocprof_same_build": same}
+
     out = {
         "metric": metric,
         "value": value,
         "unit": "GB/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": elapsed / steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -452,7 +561,7 @@ def main(argv=None):
             "decode": "per-stripe random n-k erasures, contexts built "
                       "on-GPU inside the timed step",
             "parallelism": f"stripe-sharded x{world} (no collective)",
-            "chunks": NC, "streams": len(streams),
+            "chunks": res["NC"], "streams": res["streams"],
         },
         "per_gpu_value": value / world,
         "hbm_fraction": value / world / HBM_PEAK_GBS,
@@ -461,15 +570,14 @@ def main(argv=None):
         "decode_ms": dec_ms,
         "decode_ctx_ms": ctx_ms,
         "decode_GBps": dec_gbs,
-        "roundtrip_ok": ok,
+        "roundtrip_ok": res["ok"],
         # the dominant kernel: the encode (one launch per encode call at
         # every BASELINE config: whole 1024-column tiles, no tail kernel),
         # timed by HIP events on its launch stream
-        "roofline": {
+        "roofline": dict({
             "bound": "hbm",
             "kernel": enc_kernel,
             "timed_by": "hip_events",  # around the one encode launch, on its stream
-
             "achieved": enc_gbs,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -479,13 +587,12 @@ def main(argv=None):
             "traffic_ratio": (penc["hbm_bytes_per_launch"] / (C * enc_b)
                               if penc.get("hbm_bytes_per_launch") else None),
             "valu": valu_summary(penc),
-        },
+        }, **rocprof_frac("encode", C * enc_b)),
         # the decode step (context build + matrix kernels) against the same
         # roofline: algorithmic bytes 2k * 2P per stripe
-        "decode_roofline": {
+        "decode_roofline": dict({
             "kernels": dec_kernels,
             "timed_by": "hip_events",  # context build + decode kernels, on their stream
-
             "achieved": dec_gbs,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -495,25 +602,14 @@ def main(argv=None):
             "traffic_ratio": (pdec["hbm_bytes_per_launch"] / (C * dec_b)
                               if pdec.get("hbm_bytes_per_launch") else None),
             "valu": valu_summary(pdec),
-        },
+        }, **rocprof_frac("decode", C * dec_b)),
         "pmc_source": (pmc or {}).get("source"),
         "cpu_baseline": None,
-        "build_id": None if dry else qa.build_id(),
+        "build_id": build,
     }
     if dry:
         out["dry_run"] = True
-    # the CPU baseline runs on rank 0 after the timed region and its final
-    # barrier (every rank's kernels are done), at every world size, so a
-    # multi-GPU line carries the same-run CPU number as the 1-GPU one
-    if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(k, m, P, sys_, args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist:
-        dist.barrier()  # the other ranks wait for rank 0's CPU baseline
-        dist.destroy_process_group()
-    if not ok:
-        sys.exit(3)
+    return out
 
 
 if __name__ == "__main__":

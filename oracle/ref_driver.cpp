@@ -422,7 +422,7 @@ int ref_nf4_decode_blocks(int ws, int k, int m, size_t pkt, uint8_t** data,
  * (`missing`), until `min_seconds` of wall time have passed (at least one
  * stripe each).  Returns the wall seconds of the whole job; *stripes
  * receives the stripes done by all threads together, enc_s/dec_s the
- * per-phase sums of thread 0.
+ * per-phase thread-seconds summed over all threads.
  */
 double ref_bench(int sys, int k, int m, size_t pkt, double min_seconds, int threads,
                  const int* missing, long long* stripes, double* enc_s,
@@ -485,10 +485,17 @@ double ref_bench(int sys, int k, int m, size_t pkt, double min_seconds, int thre
         total += v;
     if (stripes)
         *stripes = total;
+    // thread-seconds spent in encode / decode, summed over the threads
+    // (per stripe: / *stripes)
+    double se = 0, sd = 0;
+    for (int t = 0; t < threads; t++) {
+        se += te[t];
+        sd += td[t];
+    }
     if (enc_s)
-        *enc_s = te[0];
+        *enc_s = se;
     if (dec_s)
-        *dec_s = td[0];
+        *dec_s = sd;
     return std::chrono::duration<double>(t1 - t0).count();
 }
 

@@ -205,6 +205,8 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
 // 4-entry groups per row of a context matrix, at most
 constexpr int kPackNj = kMatMaxKin / 4;
 // rows per chunk of the non-systematic k > 128 contexts (decode_ctx_kernel):
+// (the kernel's static LDS + kCtxChunk * kMatMaxKin * 4 bytes must fit
+// kCtxLdsCap; launch_decode_ctx checks)
 // 64 rows = 4 row blocks per packing pass at 16 lanes per row (32 rows at 32
 // lanes: twice the passes and barriers for the same work; contexts k256
 // 120 -> 114 us, k300 179 -> 161 us, k384 219 -> 206 us)
@@ -212,6 +214,7 @@ constexpr int kPackNj = kMatMaxKin / 4;
 #define QI_CTX_CHUNK 64
 #endif
 constexpr int kCtxChunk = QI_CTX_CHUNK;
+constexpr int kCtxLdsCap = 160 * 1024;
 
 // One pass: NT / LPR rows from row block rb0 on (LPR lanes per row); row
 // t's canonical entries i0 .. i0 + 3 from ent(t, i0, e).  stg: a row per
@@ -379,8 +382,10 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // slow-tile list behind it starts empty
     for (long long t = tid; t < ntiles; t += NT)
         route[t * kRouteStride] = 0;
-    if (tid == 0)
+    if (tid == 0) {
         route[ntiles * kRouteStride] = 0;
+        route[lazy_word_off(words)] = 0;  // no lazily filled section yet
+    }
     if (tid < k) {
         const uint32_t id = ids[static_cast<long long>(s) * k + tid];
         xs[tid] = powm(r, id);
@@ -562,7 +567,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     if constexpr (BIG) {
         __shared__ uint32_t stg[kCtxChunk][2 * kPackNj];
         if (!dot2 && mode == 0) {
-            // whole-tile widths, non-systematic: the rows in 32-row chunks
+            // whole-tile widths, non-systematic: the rows in 64-row chunks
             // from the top, never in global memory.  Thread i runs Q_i's
             // synthetic division again (1 / A'(x_i) is known now), writing
             // the chunk's rows into LDS; then the chunk's two row blocks are
@@ -747,8 +752,10 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         cids[i] = 0;
     for (long long t = tid; t < ntiles; t += NT)
         route[t * kRouteStride] = 0;
-    if (tid == 0)
+    if (tid == 0) {
         route[ntiles * kRouteStride] = 0;  // the slow-tile list starts empty
+        route[lazy_word_off(words)] = 0;   // no lazily filled section yet
+    }
     // x_i = r^{id_i}: thread tid takes point tid (its Q chain below); wave 0
     // also point 64 + lane (its A(x) chain reads every point by readlane)
     int32_t xt = 0, xt1 = 0;
@@ -1035,9 +1042,13 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
 // a decode whose rows the matrix cores cannot address (launch_matrix then
 // runs the dot2 kernel over every column).  Decode contexts hold rows the
 // dot2 kernel can take (coef_ok), so the balanced entries fit its pairs.
-__global__ __launch_bounds__(256) void fill_dot2_kernel(MatLayout L, int32_t* ctx, long long cs)
+__global__ __launch_bounds__(256) void fill_dot2_kernel(MatLayout L, int32_t* ctx, long long cs,
+                                                        long long lazy_off)
 {
     int32_t* mat = ctx + blockIdx.x * cs;
+    uint32_t* lazy = reinterpret_cast<uint32_t*>(mat + lazy_off);
+    if (*lazy & kLazyDot2)
+        return;  // filled by an earlier decode (block-uniform)
     const int32_t* mf = mat + L.mf();
     int32_t* plain = mat + L.plain();
     for (int it = threadIdx.x; it < L.R * L.KP; it += 256) {
@@ -1054,14 +1065,19 @@ __global__ __launch_bounds__(256) void fill_dot2_kernel(MatLayout L, int32_t* ct
         mat[static_cast<size_t>(t) * L.KP + j] = static_cast<int32_t>(
             (static_cast<uint32_t>(v[0]) & 0xffffu) | (static_cast<uint32_t>(v[1]) << 16));
     }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *lazy |= kLazyDot2;
 }
 
-int fill_dot2_sections(const MatLayout& L, int32_t* d_ctx, long long ctx_stride, int S,
-                       hipStream_t st)
+int fill_dot2_sections(const MatLayout& L, int32_t* d_ctx, long long ctx_stride, long long words,
+                       int S, hipStream_t st)
 {
     if (S <= 0)
         return 0;
-    hipLaunchKernelGGL(fill_dot2_kernel, dim3(S), dim3(256), 0, st, L, d_ctx, ctx_stride);
+    const long long lazy_off = L.words() + 2LL * L.KP + lazy_word_off(words);
+    hipLaunchKernelGGL(fill_dot2_kernel, dim3(S), dim3(256), 0, st, L, d_ctx, ctx_stride,
+                       lazy_off);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1077,19 +1093,29 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
         // the matrix rows in the context itself (no LDS image); 1024 threads
         // keep 4x more of the packing and tile passes' row loads in flight
         // (k256 decode 0.81 -> 0.77 ms, k200 2.09 -> 2.05 ms)
-        // (the non-systematic whole-tile contexts stage 32-row chunks of
-        // the matrix in the dynamic LDS)
-        const size_t lds = static_cast<size_t>(kCtxChunk) * ((k + 3) & ~3) * 4;
+        // (only the non-systematic whole-tile contexts stage kCtxChunk-row
+        // chunks of the matrix in the dynamic LDS; the systematic and dot2
+        // forms keep the rows in global memory and reserve none)
+        const size_t lds = mode == 0 && !dot2
+                               ? static_cast<size_t>(kCtxChunk) * ((k + 3) & ~3) * 4
+                               : 0;
         static std::atomic<uint64_t> attr_done{0};
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess)
             return -2;
         const uint64_t bit = dev < 64 ? 1ull << dev : 0;
         if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
-            if (hipFuncSetAttribute(
-                    reinterpret_cast<const void*>(&decode_ctx_kernel<1024, true>),
-                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                    static_cast<int>(kCtxChunk * kMatMaxKin * 4)) != hipSuccess)
+            const void* fn = reinterpret_cast<const void*>(&decode_ctx_kernel<1024, true>);
+            constexpr size_t kDynMax = static_cast<size_t>(kCtxChunk) * kMatMaxKin * 4;
+            // the kernel's static LDS (the packing stage, A, x_i, ...) plus
+            // the largest chunk must fit a CU (160 KiB): an added __shared__
+            // would make every k > 256 context launch fail, so say so here
+            hipFuncAttributes fa{};
+            if (hipFuncGetAttributes(&fa, fn) != hipSuccess ||
+                fa.sharedSizeBytes + kDynMax > static_cast<size_t>(kCtxLdsCap))
+                return -2;
+            if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    static_cast<int>(kDynMax)) != hipSuccess)
                 return -2;
             attr_done.fetch_or(bit, std::memory_order_release);
         }

@@ -817,6 +817,9 @@ bool RsFnt::encode_blocks_pipe(const std::vector<uint8_t*>& data_bufs,
         return false;
     const size_t total = 2 * words;
     size_t pos = 0;
+    // one operation per block call, as the reference counts it
+    // (src/fec_base.h:1136); the pipe counts its chunks
+    const uint64_t ops = n_encode_ops;
     encode_pipe(
         [&](uint8_t* h, size_t pitch, bool& cont) {
             const size_t got = std::min(pitch, total - pos);
@@ -835,6 +838,7 @@ bool RsFnt::encode_blocks_pipe(const std::vector<uint8_t*>& data_bufs,
             });
         },
         props);
+    n_encode_ops = ops + 1;
     return true;
 }
 
@@ -847,6 +851,7 @@ bool RsFnt::decode_blocks_pipe(const std::vector<int>& ids,
         return false;
     const size_t total = 2 * words;
     size_t pos = 0;
+    const uint64_t ops = n_decode_ops;  // one per block call (src/fec_base.h:1304)
     decode_pipe(
         ids, props,
         [&](uint8_t* h, size_t pitch, bool& cont) {
@@ -865,6 +870,7 @@ bool RsFnt::decode_blocks_pipe(const std::vector<int>& ids,
                     std::memcpy(outs[i] + off, hout + i * pitch, got);
             });
         });
+    n_decode_ops = ops + 1;
     return true;
 }
 
@@ -1052,9 +1058,12 @@ void RsFnt::decode(DecodeContext& context, vec::Buffers& output,
         if (!(sys && ids[r] < n_data)) {
             const size_t pi = sys ? ids[r] - n_data : ids[r];
             if (pi < props.size())
+                // decode_prepare's window is [offset, offset + pkt_size)
+                // (src/fec_base.h:1372); marks past the Buffers' own size
+                // are ignored rather than written past it
                 for (auto const& it : props[pi].get_map())
                     if (it.second == OOR_MARK && it.first >= static_cast<size_t>(offset) &&
-                        it.first < static_cast<size_t>(offset) + size)
+                        it.first < static_cast<size_t>(offset) + std::min(size, pkt_size))
                         w[it.first - static_cast<size_t>(offset)] = 65536u;
         }
         for (size_t j = 0; j < size; j++) {

@@ -245,6 +245,12 @@ struct NttCtxArgs {
     const uint16_t* ids;  // S x k fragment ids (nullptr: 0 .. k-1)
     int32_t* ctx;
     long long cs;
+    // lazy build (ntt_build_ctx_lazy): ids as dwords at ids32 + s * cs
+    // instead of `ids`; stripes whose lazy word (lazy + s * cs) has
+    // kLazyNtt set are skipped
+    const int32_t* ids32;
+    const uint32_t* lazy;
+    uint32_t* err;        // kErrBadIds: an id >= n
 };
 
 // a * b mod q for a, b in [0, 65536] on the full-rate 24-bit multipliers:
@@ -283,9 +289,15 @@ __global__ __launch_bounds__(kNttBlock) void ntt_ctx_kernel(NttCtxArgs a)
     int32_t* C = ctx + a.L.c_off();
     int32_t* posmap = ctx + a.L.pos_off();
     int32_t* ids = ctx + a.L.ids_off();
+    if (a.lazy && (a.lazy[s * a.cs] & kLazyNtt))
+        return;  // built by an earlier decode (block-uniform)
     const uint16_t* sid = a.ids ? a.ids + static_cast<long long>(s) * k : nullptr;
+    const int32_t* sid32 = a.ids32 ? a.ids32 + s * a.cs : nullptr;
+    auto id_of = [&](int i) -> uint32_t {
+        return sid32 ? static_cast<uint32_t>(sid32[i]) : sid ? sid[i] : static_cast<uint32_t>(i);
+    };
     for (int i = tid; i < kp; i += kNttBlock)
-        xs[i] = i < k ? powm_(a.r, sid ? sid[i] : static_cast<uint32_t>(i)) : 0xffffffffu;
+        xs[i] = i < k ? powm_(a.r, id_of(i)) : 0xffffffffu;
     if (blockIdx.y == 0) {
         for (int t = tid; t < a.L.n; t += kNttBlock)
             posmap[t] = -1;
@@ -293,9 +305,12 @@ __global__ __launch_bounds__(kNttBlock) void ntt_ctx_kernel(NttCtxArgs a)
     __syncthreads();
     if (blockIdx.y == 0) {
         for (int i = tid; i < k; i += kNttBlock) {
-            const int id = sid ? sid[i] : i;
+            const int id = static_cast<int>(id_of(i));
             ids[i] = id;
-            posmap[id] = i;
+            if (id < a.L.n)
+                posmap[id] = i;
+            else
+                atomicOr(a.err, kErrBadIds);
         }
     }
     const int u = blockIdx.y * kNttBlock + tid;
@@ -324,6 +339,16 @@ __global__ __launch_bounds__(kNttBlock) void ntt_ctx_kernel(NttCtxArgs a)
         C[u] = static_cast<int32_t>(subm_(0u, mulm24(p, a.inv_len2k)));
     else
         invA[self] = static_cast<int32_t>(powm_(mulm24(p, z), 65535u));
+}
+
+// after a lazy ntt_ctx_kernel launch on the same stream: mark the stripes'
+// NTT contexts built
+__global__ __launch_bounds__(256) void lazy_mark_kernel(uint32_t* lazy, long long cs, int S,
+                                                        uint32_t bit)
+{
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s < S)
+        lazy[s * cs] |= bit;
 }
 
 // decode step 1: received row i of stripe s -> scratch row i, y = v inv_A_i
@@ -989,6 +1014,7 @@ struct ErasCtxArgs {
     const uint16_t* ids;  // S x k received ids, ascending (nullptr: 0 .. k-1)
     int32_t* ctx;
     long long cs;
+    uint32_t* err;        // the plan's sticky error word (kErrBadIds)
 };
 
 // One wave per stripe: the received bitmap, the erased list E (ascending),
@@ -1010,11 +1036,20 @@ __global__ __launch_bounds__(64) void eras_ctx_kernel(ErasCtxArgs a)
     for (int w = lane; w < nw; w += 64)
         bm[w] = 0;
     __syncthreads();
+    // ids must be distinct and < n: an id past n is dropped and a repeated
+    // one leaves more than e positions missing; either way nothing is
+    // written outside this stripe's context (the E list keeps its first e
+    // entries) and the plan's sticky error is raised
+    bool bad = false;
     for (int i = lane; i < k; i += 64) {
         const int id = sid ? sid[i] : i;
         ids[i] = id;
-        pos[id] = i;
-        atomicOr(&bm[id >> 5], 1u << (id & 31));
+        if (id < n) {
+            pos[id] = i;
+            atomicOr(&bm[id >> 5], 1u << (id & 31));
+        } else {
+            bad = true;
+        }
     }
     __syncthreads();
     // erased positions in ascending order: lane w takes bitmap word w (at
@@ -1031,11 +1066,17 @@ __global__ __launch_bounds__(64) void eras_ctx_kernel(ErasCtxArgs a)
         const int b = __ffs(miss) - 1;
         miss &= miss - 1;
         const int t = lane * 32 + b;
-        eid[off] = t;
-        ctx[a.L.eid_off() + off] = t;
-        pos[t] = -1 - off;
+        if (off < e) {
+            eid[off] = t;
+            ctx[a.L.eid_off() + off] = t;
+            pos[t] = -1 - off;
+        } else {
+            bad = true;
+        }
         off++;
     }
+    if (__builtin_amdgcn_ballot_w64(bad) && lane == 0)
+        atomicOr(a.err, kErrBadIds);
     __syncthreads();
     const uint32_t xj = lane < e ? powm_(a.rinv, static_cast<uint32_t>(eid[lane])) : 0u;
     uint32_t ad = lane == 0 ? 1u : 0u;  // A, coefficient `lane`
@@ -1837,6 +1878,20 @@ int interpolate(const qi_plan* p, const int32_t* ctx, long long cs, const RowSrc
 
 }  // namespace
 
+static int launch_ntt_ctx(const qi_plan* p, const NttCtxArgs& a, int S, hipStream_t st)
+{
+    const size_t lds =
+        static_cast<size_t>((p->k + kCtxChains - 1) / kCtxChains * kCtxChains) * 4;
+    if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_ctx_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           static_cast<int>(lds)) != hipSuccess)
+        return -2;
+    const int items = p->len2k + p->k;
+    hipLaunchKernelGGL(ntt_ctx_kernel, dim3(S, (items + kNttBlock - 1) / kNttBlock),
+                       dim3(kNttBlock), lds, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 long long ntt_ctx_words(const qi_plan* p)
 {
     return eras_plan(p) ? eras_layout(p).words() : ctx_layout_of(p).words();
@@ -1849,21 +1904,30 @@ int ntt_build_ctx(const qi_plan* p, const uint16_t* d_ids, int S, int32_t* ctx, 
         return 0;
     if (eras_plan(p)) {
         const uint32_t r = root_of_unity(static_cast<uint32_t>(p->n));
-        ErasCtxArgs e{eras_layout(p), r, invmod_c(r), d_ids, ctx, cs};
+        ErasCtxArgs e{eras_layout(p), r, invmod_c(r), d_ids, ctx, cs, p->d_err};
         hipLaunchKernelGGL(eras_ctx_kernel, dim3(S), dim3(64), 0, st, e);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     NttCtxArgs a{ctx_layout_of(p), p->r, root_of_unity(static_cast<uint32_t>(p->len2k)),
-                 invmod_c(static_cast<uint32_t>(p->len2k)), d_ids, ctx, cs};
-    const size_t lds =
-        static_cast<size_t>((p->k + kCtxChains - 1) / kCtxChains * kCtxChains) * 4;
-    if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_ctx_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           static_cast<int>(lds)) != hipSuccess)
-        return -2;
-    const int items = p->len2k + p->k;
-    hipLaunchKernelGGL(ntt_ctx_kernel, dim3(S, (items + kNttBlock - 1) / kNttBlock),
-                       dim3(kNttBlock), lds, st, a);
+                 invmod_c(static_cast<uint32_t>(p->len2k)), d_ids, ctx, cs, nullptr, nullptr,
+                 p->d_err};
+    return launch_ntt_ctx(p, a, S, st);
+}
+
+int ntt_build_ctx_lazy(const qi_plan* p, const int32_t* ids32, int S, int32_t* ctx,
+                       long long cs, uint32_t* lazy, hipStream_t st)
+{
+    if (S <= 0)
+        return 0;
+    if (eras_plan(p) || !ids32 || !lazy)
+        return -1;  // only the 256 < k <= 384 plans build lazily
+    NttCtxArgs a{ctx_layout_of(p), p->r, root_of_unity(static_cast<uint32_t>(p->len2k)),
+                 invmod_c(static_cast<uint32_t>(p->len2k)), nullptr, ctx, cs, ids32, lazy,
+                 p->d_err};
+    if (int rc = launch_ntt_ctx(p, a, S, st))
+        return rc;
+    hipLaunchKernelGGL(lazy_mark_kernel, dim3((S + 255) / 256), dim3(256), 0, st, lazy, cs, S,
+                       kLazyNtt);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

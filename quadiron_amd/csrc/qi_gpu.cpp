@@ -37,24 +37,32 @@ bool use_matrix(const qi_plan* p, long long words)
 }
 
 // the matrix-format part of a context: packed block, ids, route table,
-// slow-tile list
+// slow-tile list, lazy-section word
 long long mat_ctx_words(const qi_plan* p, long long words)
 {
     const MatLayout L = ctx_layout(p);
-    return static_cast<long long>(L.words()) + 2 * L.KP +
-           route_tiles(words) * kRouteStride + slow_words(words);
+    return static_cast<long long>(L.words()) + 2 * L.KP + lazy_word_off(words) + kLazyWords;
 }
 
 // A context built for a whole-tile width carries only the matrix-core
-// form; rows the matrix cores cannot address send every column to the dot2
-// kernel, whose sections are filled from the tiles first (idempotent)
-int complete_dot2(const qi_plan* p, const void* d_ctx, long long cs, long long words, int S,
+// form.  Rows the matrix cores cannot address send every column to the dot2
+// kernel (k <= 256), whose sections are filled from the tiles by the first
+// such decode, or to the NTT engine (256 < k <= 384), whose context is built
+// by the first such decode from the ids the matrix context holds; the
+// context's lazy word records both, so each is filled once (qi_gpu.h: a
+// decode may write its context)
+int complete_lazy(const qi_plan* p, const void* d_ctx, long long cs, long long words, int S,
                   hipStream_t s)
 {
     if (words % kRouteTile != 0)
         return 0;  // built with them
-    return fill_dot2_sections(ctx_layout(p), static_cast<int32_t*>(const_cast<void*>(d_ctx)),
-                              cs, S, s);
+    int32_t* c = static_cast<int32_t*>(const_cast<void*>(d_ctx));
+    const MatLayout L = ctx_layout(p);
+    if (p->mbig)
+        return ntt_build_ctx_lazy(
+            p, c + L.words(), S, c + mat_ctx_words(p, words), cs,
+            reinterpret_cast<uint32_t*>(c + L.words() + 2 * L.KP + lazy_word_off(words)), s);
+    return fill_dot2_sections(L, c, cs, words, S, s);
 }
 
 }  // namespace
@@ -80,9 +88,10 @@ SlowList ctx_slow(const qi_plan* p, const void* d_ctx, long long words)
 }
 
 // Decode contexts for n_stripes stripes, built on the device inside the
-// caller's stream: k <= 256, interpolation matrices + OOR route tables
-// (decode_ctx_kernel); k > 256, the NTT decode's per-pattern constants
-// (ntt_ctx_kernel; its decode reads the OOR buckets directly).
+// caller's stream: the matrix paths (k <= 256; 256 < k <= 384 at whole-tile
+// widths), interpolation matrices + OOR route tables (decode_ctx_kernel);
+// otherwise the NTT decode's per-pattern constants (ntt_ctx_kernel or
+// eras_ctx_kernel; its decode reads the OOR buckets directly).
 int build_ctx(qi_plan* p, const uint16_t* d_ids, int n_stripes, const Oor* in,
               int slot_base, int by_pos, long long words, void* d_ctx, hipStream_t s)
 {
@@ -94,13 +103,8 @@ int build_ctx(qi_plan* p, const uint16_t* d_ids, int n_stripes, const Oor* in,
     if (!use_matrix(p, words))
         return ntt_build_ctx(p, d_ids, n_stripes, static_cast<int32_t*>(d_ctx), cs, s);
     const MatLayout L = ctx_layout(p);
-    if (p->mbig) {
-        const int rc = ntt_build_ctx(p, d_ids, n_stripes,
-                                     static_cast<int32_t*>(d_ctx) + mat_ctx_words(p, words), cs,
-                                     s);
-        if (rc)
-            return rc;
-    }
+    // (256 < k <= 384: the NTT engine's half only when a decode needs it,
+    // complete_lazy)
     // the dot2 sections only for widths with a column tail (below 256 < k:
     // no dot2 kernel at all); a whole-tile decode that needs them after all
     // fills them from the tiles (qi_gpu_decode)
@@ -207,12 +211,12 @@ int qi_gpu_decode(qi_plan* p, const void* d_ctx, const uint16_t* d_ids,
         return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, p->sys ? p->k : 0, out,
                           words, n_stripes, st(stream));
     if (!matrix_cores_take(src, out, L.R, words)) {
+        if (int rc = complete_lazy(p, d_ctx, cs, words, n_stripes, st(stream)))
+            return rc;
         if (p->mbig)
             return ntt_decode(p, ctx + mat_ctx_words(p, words), cs, src,
                               d_counts ? &in : nullptr, p->sys ? p->k : 0, out, words,
                               n_stripes, st(stream));
-        if (int rc = complete_dot2(p, d_ctx, cs, words, n_stripes, st(stream)))
-            return rc;
     }
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, p->sys ? p->k : 0,
@@ -256,12 +260,12 @@ int qi_gpu_decode_packed(qi_plan* p, const void* d_ctx, const uint16_t* d_recv,
         return ntt_decode(p, ctx, cs, src, d_counts ? &in : nullptr, 0, out, words,
                           n_stripes, st(stream));
     if (!matrix_cores_take(src, out, L.R, words)) {
+        if (int rc = complete_lazy(p, d_ctx, cs, words, n_stripes, st(stream)))
+            return rc;
         if (p->mbig)
             return ntt_decode(p, ctx + mat_ctx_words(p, words), cs, src,
                               d_counts ? &in : nullptr, 0, out, words, n_stripes,
                               st(stream));
-        if (int rc = complete_dot2(p, d_ctx, cs, words, n_stripes, st(stream)))
-            return rc;
     }
     return launch_matrix(L, ctx, cs, ctx + L.words(), cs, src, out, words,
                          n_stripes, d_counts ? &in : nullptr, 0, nullptr, p->d_rowid,
@@ -287,8 +291,7 @@ const char* qi_gpu_kernels(const qi_plan* p, long long words)
             enc = matrix_kernel_names(p->gen, words, false, false);
         const MatLayout L = ctx_layout(p);
         // launch_decode_ctx's choice (ctx.hip)
-        dec = std::string(p->mbig ? "ntt_ctx_kernel + " : "") +
-              (p->k > 128  ? "decode_ctx_kernel<1024, true>"
+        dec = std::string(p->k > 128  ? "decode_ctx_kernel<1024, true>"
                : p->k > 32 ? "decode_ctx_lds_kernel<256>"
                            : "decode_ctx_lds_kernel<128>") +
               " + " + matrix_kernel_names(L, words, true, p->sys != 0);

@@ -30,6 +30,11 @@ __host__ __device__ inline long long route_tiles(long long words)
 // marks than its capacity `cap`, so some marks were lost (encode keeps the
 // exact count, decode could not restore every 65536 symbol).
 constexpr uint32_t kErrOorTruncated = 1u;
+// A decode context was asked for with received ids that are not distinct or
+// not below n (the erasure decode's context, which derives the erased set
+// from them, checks; the context is then unusable and nothing outside it is
+// written).
+constexpr uint32_t kErrBadIds = 2u;
 
 // Row source for the matrix kernel: fragment `id` of stripe `s` is at
 //   id <  split : base0 + s*ss0 + id*rs0
@@ -81,6 +86,19 @@ __host__ __device__ inline long long slow_words(long long words)
     return 1 + (words + kSlowGrain - 1) / kSlowGrain;
 }
 
+// A matrix context's lazy-section word (behind its slow-tile list, per
+// stripe, cleared by the context builder): the sections a decode fills on
+// first use, when the batch's rows keep it off the matrix cores -- bit 0
+// the dot2 sections (fill_dot2_sections), bit 1 the NTT engine's context of
+// a 256 < k <= 384 plan (ntt_build_ctx_lazy).  Offset from the route table.
+constexpr uint32_t kLazyDot2 = 1u, kLazyNtt = 2u;
+__host__ __device__ inline long long lazy_word_off(long long words)
+{
+    return route_tiles(words) * kRouteStride + slow_words(words);
+}
+// words reserved for it (keeps the following section's alignment)
+constexpr int kLazyWords = 4;
+
 // ---- launchers (kernels.hip) ----
 // non-systematic encode by twisted register-resident sub-NTTs
 int launch_encode_fnt(int k, int n, int n_out, const int32_t* d_twist,
@@ -113,7 +131,8 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long mat_stride,
 //   d_ctx: per stripe ctx_stride words: the MatLayout block, the k ids as
 //   int32 (padded to 2 KP), the OOR route table (route_tiles(words) x
 //   kRouteStride u32) built from in_oor, then the slow-tile list
-//   (slow_words(words) u32, count cleared)
+//   (slow_words(words) u32, count cleared), then the lazy-section word
+//   (cleared; lazy_word_off)
 //   (slot = by_pos ? position : id - slot_base); in_oor may be null.
 //   n: the code length (ids < n), r its root of unity
 //   dot2: also write the dot2 kernel's sections (packed pairs, `plain`
@@ -123,10 +142,12 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
                       long long ctx_stride, const Oor* in_oor, int slot_base,
                       int by_pos, long long words, int dot2, uint32_t* d_err,
                       hipStream_t stream);
-// the dot2 sections of n_stripes contexts built with dot2 = 0, from their
-// operand tiles (before a decode that runs the dot2 kernel over them)
-int fill_dot2_sections(const MatLayout& L, int32_t* d_ctx, long long ctx_stride, int n_stripes,
-                       hipStream_t stream);
+// the dot2 sections of n_stripes contexts built with dot2 = 0 for `words`
+// columns, from their operand tiles (before a decode that runs the dot2
+// kernel over them); a stripe whose lazy word has kLazyDot2 set is skipped,
+// and the bit is set after the fill
+int fill_dot2_sections(const MatLayout& L, int32_t* d_ctx, long long ctx_stride, long long words,
+                       int n_stripes, hipStream_t stream);
 
 // matrix kernel instantiation choice
 int matrix_kp(int kin);

@@ -106,6 +106,12 @@ void ntt_plan_free(qi_plan* p);
 long long ntt_ctx_words(const qi_plan* p);
 int ntt_build_ctx(const qi_plan* p, const uint16_t* d_ids, int n_stripes, int32_t* d_ctx,
                   long long ctx_stride, hipStream_t s);
+// the same from ids held as dwords (ids32 + s * ids_stride: a matrix
+// context's id section), skipping the stripes whose lazy word (lazy + s *
+// ctx_stride) has kLazyNtt set and setting it after: a 256 < k <= 384
+// decode builds its NTT context only when the matrix cores cannot take it
+int ntt_build_ctx_lazy(const qi_plan* p, const int32_t* ids32, int n_stripes, int32_t* d_ctx,
+                       long long ctx_stride, uint32_t* lazy, hipStream_t s);
 int ntt_encode(const qi_plan* p, const uint16_t* data, long long dss, long long drs,
                RowDst out, long long words, int n_stripes, const Oor* oor, hipStream_t s);
 int ntt_decode(const qi_plan* p, const int32_t* ctx, long long ctx_stride, RowSrc src,

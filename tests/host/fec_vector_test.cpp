@@ -161,6 +161,43 @@ static void run_buffers(FecType type, unsigned k, unsigned m, size_t size, unsig
                    "decode row %u col %zu (type %d)", i, j, static_cast<int>(type));
 }
 
+// A block wider than one pipeline chunk (4 MiB per fragment) goes through
+// the two-slot pipeline chunk by chunk, yet counts as ONE operation per
+// block call, as the reference counts it (src/fec_base.h:1136, 1304;
+// ADVICE r4), and round-trips.
+static void run_block_ops()
+{
+    const unsigned k = 4, m = 4;
+    const size_t bytes = 10u << 20;  // three chunks
+    RsFnt fec(FecType::NON_SYSTEMATIC, 2, k, m);
+    const unsigned no = static_cast<unsigned>(fec.get_n_outputs());
+    std::vector<std::vector<uint8_t>> data(k, std::vector<uint8_t>(bytes)),
+        coded(no, std::vector<uint8_t>(bytes)), out(k, std::vector<uint8_t>(bytes));
+    std::mt19937 rng(7);
+    for (auto& d : data)
+        for (auto& b : d)
+            b = static_cast<uint8_t>(rng());
+    std::vector<uint8_t*> dp(k), cp(no), op(k);
+    for (unsigned i = 0; i < k; i++) {
+        dp[i] = data[i].data();
+        op[i] = out[i].data();
+    }
+    for (unsigned i = 0; i < no; i++)
+        cp[i] = coded[i].data();
+    std::vector<Properties> props(no);
+    std::vector<bool> wanted(no, true);
+    fec.encode_blocks_vertical(dp, cp, props, wanted, bytes);
+    EXPECT(fec.n_encode_ops == 1, "encode ops %llu", (unsigned long long)fec.n_encode_ops);
+    std::vector<int> missing(k + m, 0);
+    missing[0] = missing[2] = missing[5] = 1;  // decode from 1, 3, 4, 6
+    std::vector<bool> want(k, true);
+    fec.reset_stats_dec();
+    EXPECT(fec.decode_blocks_vertical(op, cp, props, missing, want, bytes), "decode");
+    EXPECT(fec.n_decode_ops == 1, "decode ops %llu", (unsigned long long)fec.n_decode_ops);
+    for (unsigned i = 0; i < k; i++)
+        EXPECT(out[i] == data[i], "block round trip, row %u", i);
+}
+
 int main()
 {
     run_test(FecType::NON_SYSTEMATIC, 1);  // TestFnt
@@ -169,6 +206,7 @@ int main()
     run_buffers(FecType::SYSTEMATIC, 3, 3, 1000, 4);
     run_buffers(FecType::NON_SYSTEMATIC, 16, 48, 4096, 5);
     run_buffers(FecType::SYSTEMATIC, 10, 6, 3000, 6);
+    run_block_ops();
     if (fails) {
         std::fprintf(stderr, "%d failures\n", fails);
         return 1;

@@ -545,6 +545,23 @@ def test_unaligned_rows_whole_tiles(k, m, sys_):
                        entries=entries, cap=cap) == 0
     torch.cuda.synchronize()
     assert torch.equal(dec2, dd)
+    # a second unaligned decode reuses the sections the first one filled
+    # (the context's lazy word)
+    dec.zero_()
+    assert plan.decode(ctx, di, out, dec, data=dd, counts=counts, entries=entries,
+                       cap=cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec, dd)
+    # other patterns built into the same buffer: the builder clears the lazy
+    # word, so the next unaligned decode fills the sections again
+    ids2 = np.stack([np.sort(rng.choice(k + m, k, replace=False)) for _ in range(S)])
+    di2 = torch.from_numpy(ids2.astype(np.uint16).view(np.int16)).cuda()
+    plan.decode_ctx(di2, ctx, P, counts, entries, cap)
+    dec.zero_()
+    assert plan.decode(ctx, di2, out, dec, data=dd, counts=counts, entries=entries,
+                       cap=cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec, dd)
 
 
 def test_big_matrix_ctx_sized_for_a_wider_batch():
@@ -752,6 +769,42 @@ def test_decode_bucket_overflow_raises(k, m):
     assert plan.decode(ctx, di, out, dec, counts=counts, entries=entries,
                        cap=cap) != 0
     assert plan.take_error() == 0  # reset by reading
+
+
+@pytest.mark.parametrize("bad", ["repeated", "past_n"])
+def test_erasure_ctx_bad_ids_raise(bad):
+    """The erasure decode's context (k > 384, n - k <= 64) derives the erased
+    set from the received ids.  A repeated id (more than n - k positions
+    then look erased) or an id >= n must raise the plan's sticky error and
+    write nothing outside the stripe's own context: the next stripe's
+    context is the one it builds alone, and guard bytes behind the buffer
+    stay untouched."""
+    torch = _torch()
+    import quadiron_amd as qa
+    k, m, S, P = 500, 10, 2, 64
+    plan = qa.Plan(k, m, False)
+    assert "ntt_eras_kernel" in plan.kernels(P)
+    rng = np.random.default_rng(3)
+    ids = np.stack([np.sort(rng.choice(k + m, k, replace=False))
+                    for _ in range(S)]).astype(np.uint16)
+    if bad == "repeated":
+        ids[0, 7] = ids[0, 6]
+    else:
+        ids[0, -1] = 600  # n = 512
+    di = torch.from_numpy(ids.view(np.int16)).cuda()
+    nb = plan.ctx_bytes(S, P)
+    cs = plan.ctx_bytes(1, P)
+    buf = torch.full((nb + 4096,), 0x5A, dtype=torch.uint8, device="cuda")
+    plan.decode_ctx(di, buf[:nb], P)
+    torch.cuda.synchronize()
+    assert plan.take_error() != 0
+    assert plan.take_error() == 0  # reset by reading
+    assert bool((buf[nb:] == 0x5A).all())
+    one = torch.full((cs,), 0x5A, dtype=torch.uint8, device="cuda")
+    plan.decode_ctx(di[1:], one, P)
+    torch.cuda.synchronize()
+    assert plan.take_error() == 0
+    assert torch.equal(buf[cs:2 * cs], one)
 
 
 def test_plan_argument_checks():

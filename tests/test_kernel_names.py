@@ -46,3 +46,7 @@ def test_reported_kernels_exist(cfg, sys_):
     dec = kernels.split("; ")[1]
     assert "ctx_" in dec.split(" + ")[0] or dec.startswith("decode=ntt_ctx_kernel")
 
+    # 256 < k <= 384 at whole-tile widths: the NTT engine's context is built
+    # only by a decode the matrix cores cannot take
+    if cfg in ("k300", "k384"):
+        assert "ntt_ctx_kernel" not in dec, kernels

@@ -1,0 +1,246 @@
+// cfg3-encode probe ladder (not part of the product): the memory shape of
+// matrix_mfma_kernel<4,8,4,true> (1024 stripes, 64 input rows and 1024 output
+// rows of 4 KiB, a block of 4 waves on 512 columns of one stripe, XCD-grouped
+// block map, stores of 8 rows x 128 B) with the kernel's other phases added
+// one at a time, to attribute the gap between the bare store shape and the
+// kernel without its epilogue math:
+//   L0  row loads to registers, then every store (tools/membw5.hip RPI 8)
+//   L1  + the rows staged in LDS as byte planes (perm + xor, the product's
+//       column permutation) and a block barrier
+//   L2  + each 16 x 64 output tile transposed through the wave's LDS staging
+//       tile (2 ds_write_b128, wave barrier, 2 ds_read_b128) before its stores
+//   L3  + the operand tiles of each row block loaded from a 256 KB generator
+//       (L2-resident), one row block ahead in ping-pong, as the product
+//   L4  + 16 ds_read_b64_tr_b8 + 16 v_mfma_i32_16x16x64_i8 per output tile
+// RS > 1: a block covers 1024 / RS output rows (RS blocks per column tile,
+// consecutive on one XCD, re-staging the same input through L2).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/membw7.hip -o build/membw7
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#define CHECK(x)                                                             \
+    do {                                                                     \
+        hipError_t e = (x);                                                  \
+        if (e != hipSuccess) {                                               \
+            printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__);          \
+            exit(1);                                                         \
+        }                                                                    \
+    } while (0)
+constexpr long P = 2048;     // u16 words per row
+constexpr int KIN = 64, NOUT = 1024, TW = 512;
+constexpr int RSB = TW + 16;                     // image row pitch (bytes)
+constexpr int IMG = 2 * KIN * RSB;               // 67,584 B
+constexpr int STGP = 144, STG = 16 * STGP;       // per-wave staging tile
+constexpr int LDS = IMG + 2048 + 16 + 4 * STG;   // the product's footprint
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                             (int)bytes, 0x00020000);
+}
+template <int LV, int RS>
+__global__ __launch_bounds__(256) void enc(const uint16_t* in, uint16_t* out,
+                                           const int* gen, int tiles)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    // XCD-grouped map over (stripe, tile, row part): XCD x walks all column
+    // tiles and row parts of stripe 8 g + x
+    const int b = blockIdx.x;
+    const int j = b >> 3;
+    const int per = tiles * RS;
+    const int g8 = j / per;
+    const int s = g8 * 8 + (b & 7);
+    const int rem = j - g8 * per;
+    const int tile = rem / RS, part = rem % RS;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int tl = l & 15, gq = l >> 4;
+    auto ri = rsrc(in + (long)s * KIN * P, KIN * P * 2);
+    auto ro = rsrc(out + (long)s * NOUT * P, NOUT * P * 2);
+    // staging: thread t loads 2 columns (b32) of all 64 rows
+    const uint32_t cl = threadIdx.x * 2;
+    const uint32_t voff = (tile * TW + cl) * 2;
+    uint32_t wv[KIN];
+#pragma unroll
+    for (int r = 0; r < KIN; r++)
+        wv[r] = __builtin_amdgcn_raw_buffer_load_b32(ri, voff, r * P * 2, 2);
+    uint32_t acc = 0;
+    if constexpr (LV == 0) {
+#pragma unroll
+        for (int r = 0; r < KIN; r++)
+            acc ^= wv[r];
+    } else {
+        const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) +
+                              4 * ((cl % 64) / 16) + cl % 4;
+#pragma unroll
+        for (int r = 0; r < KIN; r++) {
+            const uint32_t hi = __builtin_amdgcn_perm(0u, wv[r], 0x0c0c0301u) ^ 0x8080u;
+            const uint32_t lo = __builtin_amdgcn_perm(0u, wv[r], 0x0c0c0200u) ^ 0x8080u;
+            *reinterpret_cast<uint16_t*>(lds + r * RSB + lpos) = (uint16_t)hi;
+            *reinterpret_cast<uint16_t*>(lds + (KIN + r) * RSB + lpos) = (uint16_t)lo;
+        }
+        __syncthreads();
+        acc = *reinterpret_cast<const uint32_t*>(lds + l * 4);
+    }
+    // operands (L3+): the product's load_ops per row block
+    auto load_ops = [&](int rb, v2i (&bo)[4][3], int (&sc)[5]) {
+        rb = rb < 63 ? rb : 63;  // the clamped prefetch past the last row block
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++)
+#pragma unroll
+            for (int ty = 0; ty < 2; ty++)
+                bo[ks][ty] = *reinterpret_cast<const v2i*>(gen + ((rb * 4 + ks) * 3 + ty) * 128 + l * 2);
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++)
+            bo[ks][2] = ks < 2 ? bo[ks + 2][1] : bo[ks - 2][0];
+        const int t = 16 * rb + tl;
+        const int* tail = gen + 64 * 4 * 3 * 128;
+        sc[0] = tail[t];
+        sc[1] = tail[1024 + t];
+        sc[2] = tail[2048 + t];
+        sc[3] = tail[2048 + 16 * rb + (l >> 3)];
+        sc[4] = tail[2048 + 16 * rb + 8 + (l >> 3)];
+    };
+    auto* ldsa = (__attribute__((address_space(3))) uint8_t*)lds;
+    const uint32_t abase = (uint32_t)((8 * gq + ((l & 15) >> 1)) * RSB + 8 * (l & 1));
+    uint8_t* stg = lds + IMG + 2048 + 16 + w * STG;
+    constexpr int NRB = 16 / RS;  // row blocks per wave
+    auto rb_body = [&](int rb, const v2i (&bo)[4][3], const int (&sc)[5]) {
+        uint32_t x = acc;
+        if constexpr (LV >= 3)
+            x ^= (uint32_t)(bo[0][0].x ^ bo[3][1].y ^ sc[0] ^ sc[1] ^ sc[2]);
+#pragma unroll 1
+        for (int st = 0; st < 8; st++) {
+            v4u o0 = {x + st, x ^ st, x + rb, x}, o1 = {x ^ rb, x + 7, x, x ^ st};
+            if constexpr (LV >= 4) {
+                v4i a4[4][3];
+#pragma unroll
+                for (int T = 0; T < 4; T++) {
+                    a4[T][0] = v4i{0, 0, 0, 0};
+                    a4[T][1] = v4i{sc[0], sc[0], sc[0], sc[0]};
+                    a4[T][2] = v4i{0, 0, 0, 0};
+#pragma unroll
+                    for (int ks = 0; ks < 4; ks += 2) {
+                        auto rd = [&](int k2) {
+                            auto* pa = (__attribute__((address_space(3))) v2i*)(
+                                ldsa + abase + 32 * k2 * RSB + (4 * st + T) * 16);
+                            return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
+                        };
+                        const v2i p0 = rd(ks), p1 = rd(ks + 1);
+                        const v4i a{p0.x, p0.y, p1.x, p1.y};
+#pragma unroll
+                        for (int ty = 0; ty < 3; ty++) {
+                            if ((ty == 0 && ks >= 2) || (ty == 1 && ks + 1 < 2))
+                                continue;
+                            const v4i bb{bo[ks][ty].x, bo[ks][ty].y, bo[ks + 1][ty].x,
+                                         bo[ks + 1][ty].y};
+                            a4[T][ty] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bb, a4[T][ty], 0, 0, 0);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int T = 0; T < 4; T++) {
+                    o0[T] ^= (uint32_t)(a4[T][0][0] + a4[T][1][1] + a4[T][2][2]);
+                    o1[T] ^= (uint32_t)(a4[T][0][3] + a4[T][1][2] + a4[T][2][1]);
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int orow = 8 * h + (l >> 3), c = l & 7;
+                v4u v = h ? o1 : o0;
+                if constexpr (LV >= 2) {
+                    if (h == 0) {
+                        *reinterpret_cast<v4u*>(stg + tl * STGP + 32 * gq) = o0;
+                        *reinterpret_cast<v4u*>(stg + tl * STGP + 32 * gq + 16) = o1;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    }
+                    v = *reinterpret_cast<const v4u*>(stg + orow * STGP + 16 * c);
+                }
+                const int row = 16 * rb + orow;
+                int rowo = row;
+                if constexpr (LV >= 3)
+                    rowo = (sc[3 + h] & 0) + row;  // the rowmap's value, identity
+                const uint32_t vo = rowo * P * 2 + tile * TW * 2 + 128 * st + 16 * c;
+                __builtin_amdgcn_raw_buffer_store_b128(v, ro, vo, 0, 18);
+            }
+            if constexpr (LV >= 2) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    };
+    const int rbase = part * (64 / RS);
+    v2i bA[4][3], bB[4][3];
+    int sA[5], sB[5];
+    if constexpr (LV >= 3)
+        load_ops(rbase + w, bA, sA);
+    for (int jj = 0; jj < NRB; jj += 2) {
+        const int rb = rbase + w + 4 * jj;
+        if constexpr (LV >= 3)
+            load_ops(rb + 4, bB, sB);
+        rb_body(rb, bA, sA);
+        if (jj + 1 >= NRB)
+            break;
+        if constexpr (LV >= 3)
+            load_ops(jj + 2 < NRB ? rb + 8 : rb + 4, bA, sA);
+        rb_body(rb + 4, bB, sB);
+    }
+}
+template <typename F>
+float timeit(F f, int reps)
+{
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    f();
+    CHECK(hipEventRecord(a));
+    for (int r = 0; r < reps; r++)
+        f();
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+int main(int argc, char** argv)
+{
+    const int S = argc > 1 ? atoi(argv[1]) : 1024;
+    const int reps = 10;
+    uint16_t *a, *b;
+    int* gen;
+    const size_t ab = (size_t)S * KIN * P * 2, bb = (size_t)S * NOUT * P * 2;
+    const size_t gb = (64 * 4 * 3 * 128 + 4096) * 4;
+    CHECK(hipMalloc(&a, ab));
+    CHECK(hipMalloc(&b, bb));
+    CHECK(hipMalloc(&gen, gb));
+    CHECK(hipMemset(a, 1, ab));
+    CHECK(hipMemset(b, 2, bb));
+    CHECK(hipMemset(gen, 0, gb));
+    const double eb = ab + bb;
+    const int tiles = P / TW;
+#define RUN(LV, RS)                                                                        \
+    {                                                                                      \
+        CHECK(hipFuncSetAttribute((const void*)enc<LV, RS>,                               \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS));       \
+        float ms = timeit([&] { enc<LV, RS><<<tiles * S * RS, 256, LDS>>>(a, b, gen, tiles); }, \
+                          reps);                                                           \
+        CHECK(hipGetLastError());                                                          \
+        printf("cfg3 ladder L%d RS%d %7.3f ms %7.1f GB/s\n", LV, RS, ms, eb / ms / 1e6);  \
+    }
+    for (int rep = 0; rep < 2; rep++) {
+        printf("--- rep %d\n", rep);
+        RUN(0, 1)
+        RUN(1, 1)
+        RUN(2, 1)
+        RUN(3, 1)
+        RUN(4, 1)
+        RUN(0, 2)
+        RUN(4, 2)
+        RUN(0, 4)
+        RUN(4, 4)
+    }
+    return 0;
+}
