@@ -1058,12 +1058,16 @@ void RsFnt::decode(DecodeContext& context, vec::Buffers& output,
         if (!(sys && ids[r] < n_data)) {
             const size_t pi = sys ? ids[r] - n_data : ids[r];
             if (pi < props.size())
-                // decode_prepare's window is [offset, offset + pkt_size)
-                // (src/fec_base.h:1372); marks past the Buffers' own size
-                // are ignored rather than written past it
+                // decode_prepare restores the marks in [offset, offset +
+                // pkt_size) (src/fec_base.h:1372), which equals the Buffers'
+                // size on the reference's own paths; here the window is the
+                // Buffers' size: a Buffers wider than pkt_size keeps every
+                // mark (the reference would drop those past pkt_size) and a
+                // narrower one is never written past its end (deliberate
+                // deviation)
                 for (auto const& it : props[pi].get_map())
                     if (it.second == OOR_MARK && it.first >= static_cast<size_t>(offset) &&
-                        it.first < static_cast<size_t>(offset) + std::min(size, pkt_size))
+                        it.first < static_cast<size_t>(offset) + size)
                         w[it.first - static_cast<size_t>(offset)] = 65536u;
         }
         for (size_t j = 0; j < size; j++) {

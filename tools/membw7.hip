@@ -12,12 +12,17 @@
 //   L3  + the operand tiles of each row block loaded from a 256 KB generator
 //       (L2-resident), one row block ahead in ping-pong, as the product
 //   L4  + 16 ds_read_b64_tr_b8 + 16 v_mfma_i32_16x16x64_i8 per output tile
+//   L5  + the epilogue's element math (the product's kernel without its
+//       mark / row-scale paths and the pipelined pair loop)
+// and enc_as, the A-stationary alternative (below).
 // RS > 1: a block covers 1024 / RS output rows (RS blocks per column tile,
 // consecutive on one XCD, re-staging the same input through L2).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/membw7.hip -o build/membw7
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+
+#include "../quadiron_amd/csrc/gf65537.h"
 #define CHECK(x)                                                             \
     do {                                                                     \
         hipError_t e = (x);                                                  \
@@ -40,6 +45,35 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
                                              (int)bytes, 0x00020000);
 }
+// the product's epilogue element math of one 16 x 64 tile (y = 256 D2 +
+// D1 - D0 folded twice, the OOR test, packing) into o0 / o1
+__device__ __forceinline__ void epilogue(const v4i (&a4)[4][3], v4u& o0, v4u& o1)
+{
+    int32_t y[16];
+#pragma unroll
+    for (int T = 0; T < 4; T++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            y[4 * T + j] = qi::fold(qi::fold((a4[T][2][j] << 8) + a4[T][1][j] - a4[T][0][j]));
+    uint32_t bad = 0;
+#pragma unroll
+    for (int c = 0; c < 16; c++)
+        bad |= static_cast<uint32_t>(y[c]);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64((bad >> 16) != 0) != 0, 0)) {
+#pragma unroll
+        for (int c = 0; c < 16; c++)
+            if (static_cast<uint32_t>(y[c]) > 65535u)
+                y[c] = 0;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        o0[c] = __builtin_amdgcn_perm(static_cast<uint32_t>(y[2 * c + 1]),
+                                      static_cast<uint32_t>(y[2 * c]), 0x05040100u);
+        o1[c] = __builtin_amdgcn_perm(static_cast<uint32_t>(y[8 + 2 * c + 1]),
+                                      static_cast<uint32_t>(y[8 + 2 * c]), 0x05040100u);
+    }
+}
+
 template <int LV, int RS>
 __global__ __launch_bounds__(256) void enc(const uint16_t* in, uint16_t* out,
                                            const int* gen, int tiles)
@@ -139,10 +173,14 @@ __global__ __launch_bounds__(256) void enc(const uint16_t* in, uint16_t* out,
                         }
                     }
                 }
+                if constexpr (LV >= 5) {
+                    epilogue(a4, o0, o1);
+                } else {
 #pragma unroll
-                for (int T = 0; T < 4; T++) {
-                    o0[T] ^= (uint32_t)(a4[T][0][0] + a4[T][1][1] + a4[T][2][2]);
-                    o1[T] ^= (uint32_t)(a4[T][0][3] + a4[T][1][2] + a4[T][2][1]);
+                    for (int T = 0; T < 4; T++) {
+                        o0[T] ^= (uint32_t)(a4[T][0][0] + a4[T][1][1] + a4[T][2][2]);
+                        o1[T] ^= (uint32_t)(a4[T][0][3] + a4[T][1][2] + a4[T][2][1]);
+                    }
                 }
             }
 #pragma unroll
@@ -189,6 +227,121 @@ __global__ __launch_bounds__(256) void enc(const uint16_t* in, uint16_t* out,
         rb_body(rb + 4, bB, sB);
     }
 }
+// A-stationary geometry: a block of 4 waves on 256 columns of one stripe,
+// wave w owns super tile w (its A operand -- 64 columns x 128 byte-plane
+// rows, 8 v4i -- read once from the staged image into registers) and walks
+// all 64 row blocks, the generator's operand tiles of each row block loaded
+// (L2) one row block ahead.  The image is dead after the A reads and holds
+// the waves' output staging tiles; 35 KB of LDS: 4 blocks (16 waves) per CU.
+// EPI: the product's epilogue math (else a stand-in xor)
+constexpr int TWA = 256, RSBA = TWA + 16, IMGA = 2 * KIN * RSBA;
+template <bool EPI>
+__global__ __launch_bounds__(256) void enc_as(const uint16_t* in, uint16_t* out, const int* gen,
+                                              int tiles)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int b = blockIdx.x;
+    const int j = b >> 3;
+    const int g8 = j / tiles;
+    const int s = g8 * 8 + (b & 7);
+    const int tile = j - g8 * tiles;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int tl = l & 15, gq = l >> 4;
+    auto ri = rsrc(in + (long)s * KIN * P, KIN * P * 2);
+    auto ro = rsrc(out + (long)s * NOUT * P, NOUT * P * 2);
+    // staging: lane l of wave w loads 4 columns (b64) of rows w + 4 r
+    const uint32_t cl = l * 4;
+    const uint32_t voff = (tile * TWA + cl) * 2;
+    uint32_t wv[16][2];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(ri, voff, (4 * r + w) * P * 2, 2);
+        wv[r][0] = v[0];
+        wv[r][1] = v[1];
+    }
+    const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) + 4 * ((cl % 64) / 16);
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int i = 4 * r + w;
+        const uint32_t hi = __builtin_amdgcn_perm(wv[r][1], wv[r][0], 0x07050301u) ^ 0x80808080u;
+        const uint32_t lo = __builtin_amdgcn_perm(wv[r][1], wv[r][0], 0x06040200u) ^ 0x80808080u;
+        *reinterpret_cast<uint32_t*>(lds + i * RSBA + lpos) = hi;
+        *reinterpret_cast<uint32_t*>(lds + (KIN + i) * RSBA + lpos) = lo;
+    }
+    __syncthreads();
+    auto* ldsa = (__attribute__((address_space(3))) uint8_t*)lds;
+    const uint32_t abase = (uint32_t)((8 * gq + ((l & 15) >> 1)) * RSBA + 8 * (l & 1));
+    v4i av[4][2];
+#pragma unroll
+    for (int T = 0; T < 4; T++)
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            auto rd = [&](int ks) {
+                auto* pa = (__attribute__((address_space(3))) v2i*)(ldsa + abase + 32 * ks * RSBA +
+                                                                   (4 * w + T) * 16);
+                return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
+            };
+            const v2i p0 = rd(2 * kk), p1 = rd(2 * kk + 1);
+            av[T][kk] = v4i{p0.x, p0.y, p1.x, p1.y};
+        }
+    __syncthreads();  // the image is dead: it holds the staging tiles now
+    uint8_t* stg = lds + w * STG;
+    const int* tail = gen + 64 * 4 * 3 * 128;
+    auto ld_b = [&](int rb, v4i& b0, v4i& b1, int& kt) {
+        auto ld2 = [&](int ks, int ty) {
+            return *reinterpret_cast<const v2i*>(gen + ((rb * 4 + ks) * 3 + ty) * 128 + l * 2);
+        };
+        const v2i x0 = ld2(0, 0), x1 = ld2(1, 0), y0 = ld2(2, 1), y1 = ld2(3, 1);
+        b0 = v4i{x0.x, x0.y, x1.x, x1.y};
+        b1 = v4i{y0.x, y0.y, y1.x, y1.y};
+        kt = tail[16 * rb + tl];
+    };
+    v4i bA0, bA1, bB0, bB1;
+    int ktA, ktB;
+    ld_b(0, bA0, bA1, ktA);
+    auto rb_body = [&](int rb, const v4i& b0, const v4i& b1, int kt) {
+        v4i a4[4][3];
+#pragma unroll
+        for (int T = 0; T < 4; T++) {
+            a4[T][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[T][0], b0, v4i{0, 0, 0, 0}, 0, 0, 0);
+            a4[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[T][1], b1, v4i{kt, kt, kt, kt}, 0, 0, 0);
+            a4[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[T][0], b1, v4i{0, 0, 0, 0}, 0, 0, 0);
+            a4[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[T][1], b0, a4[T][2], 0, 0, 0);
+        }
+        v4u o0, o1;
+        if constexpr (EPI) {
+            epilogue(a4, o0, o1);
+        } else {
+#pragma unroll
+            for (int T = 0; T < 4; T++) {
+                o0[T] = (uint32_t)(a4[T][0][0] + a4[T][1][1] + a4[T][2][2]);
+                o1[T] = (uint32_t)(a4[T][0][3] + a4[T][1][2] + a4[T][2][1]);
+            }
+        }
+        *reinterpret_cast<v4u*>(stg + tl * STGP + 32 * gq) = o0;
+        *reinterpret_cast<v4u*>(stg + tl * STGP + 32 * gq + 16) = o1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int orow = 8 * h + (l >> 3), c = l & 7;
+            const v4u v = *reinterpret_cast<const v4u*>(stg + orow * STGP + 16 * c);
+            const uint32_t vo = (16 * rb + orow) * P * 2 + (tile * TWA + 64 * w) * 2 + 16 * c;
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, vo, 0, 18);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    };
+#pragma unroll 1
+    for (int rb = 0; rb < 64; rb += 2) {
+        ld_b(rb + 1, bB0, bB1, ktB);
+        rb_body(rb, bA0, bA1, ktA);
+        ld_b(rb + 2 < 64 ? rb + 2 : 63, bA0, bA1, ktA);
+        rb_body(rb + 1, bB0, bB1, ktB);
+    }
+}
+
 template <typename F>
 float timeit(F f, int reps)
 {
@@ -230,6 +383,13 @@ int main(int argc, char** argv)
         CHECK(hipGetLastError());                                                          \
         printf("cfg3 ladder L%d RS%d %7.3f ms %7.1f GB/s\n", LV, RS, ms, eb / ms / 1e6);  \
     }
+#define RUNAS(EPI)                                                                         \
+    {                                                                                      \
+        float ms = timeit([&] { enc_as<EPI><<<(P / TWA) * S, 256, IMGA>>>(a, b, gen, P / TWA); }, \
+                          reps);                                                           \
+        CHECK(hipGetLastError());                                                          \
+        printf("cfg3 A-stationary epi%d  %7.3f ms %7.1f GB/s\n", EPI, ms, eb / ms / 1e6);  \
+    }
     for (int rep = 0; rep < 2; rep++) {
         printf("--- rep %d\n", rep);
         RUN(0, 1)
@@ -237,10 +397,12 @@ int main(int argc, char** argv)
         RUN(2, 1)
         RUN(3, 1)
         RUN(4, 1)
-        RUN(0, 2)
-        RUN(4, 2)
+        RUN(5, 1)
         RUN(0, 4)
         RUN(4, 4)
+        RUN(5, 4)
+        RUNAS(false)
+        RUNAS(true)
     }
     return 0;
 }
