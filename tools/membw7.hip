@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "../quadiron_amd/csrc/gf65537.h"
 #define CHECK(x)                                                             \
@@ -342,6 +343,101 @@ __global__ __launch_bounds__(256) void enc_as(const uint16_t* in, uint16_t* out,
     }
 }
 
+// Half-line output stores (no LDS transpose): lane (g, t) holds row t,
+// columns {8g .. 8g+7} (o0) and {32+8g .. 32+8g+7} (o1) of a super tile (an
+// image column order that puts them there), so a store instruction of o0
+// writes 16 rows x 64 contiguous bytes, and o1 the other half of each line.
+// NW waves per block on 512 columns, wave w takes row blocks w + NW j; no
+// staging tiles: 70 KB of LDS, so 2 blocks of 8 waves (4 waves per SIMD)
+// fit a CU.  MATH: the kernel's A reads, MFMAs and epilogue (else only the
+// stores).  AUX: store policy.
+template <int NW, bool MATH, int AUX>
+__global__ __launch_bounds__(64 * NW) void enc_h(const uint16_t* in, uint16_t* out, const int* gen,
+                                                int tiles)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int b = blockIdx.x;
+    const int j = b >> 3;
+    const int g8 = j / tiles;
+    const int s = g8 * 8 + (b & 7);
+    const int tile = j - g8 * tiles;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int tl = l & 15, gq = l >> 4;
+    auto ri = rsrc(in + (long)s * KIN * P, KIN * P * 2);
+    auto ro = rsrc(out + (long)s * NOUT * P, NOUT * P * 2);
+    // staging: 256 lanes per row pass (2 columns, b32), NW / 4 row groups
+    constexpr int RG = NW / 4, RPT = KIN / RG;
+    const int rg = threadIdx.x / 256;
+    const uint32_t cl = (threadIdx.x % 256) * 2;
+    const uint32_t voff = (tile * TW + cl) * 2;
+    uint32_t wv[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; r++)
+        wv[r] = __builtin_amdgcn_raw_buffer_load_b32(ri, voff, (RG * r + rg) * P * 2, 2);
+    const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) + 4 * ((cl % 64) / 16) + cl % 4;
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+        const int i = RG * r + rg;
+        const uint32_t hi = __builtin_amdgcn_perm(0u, wv[r], 0x0c0c0301u) ^ 0x8080u;
+        const uint32_t lo = __builtin_amdgcn_perm(0u, wv[r], 0x0c0c0200u) ^ 0x8080u;
+        *reinterpret_cast<uint16_t*>(lds + i * RSB + lpos) = (uint16_t)hi;
+        *reinterpret_cast<uint16_t*>(lds + (KIN + i) * RSB + lpos) = (uint16_t)lo;
+    }
+    __syncthreads();
+    uint32_t acc = *reinterpret_cast<const uint32_t*>(lds + l * 4);
+    auto* ldsa = (__attribute__((address_space(3))) uint8_t*)lds;
+    const uint32_t abase = (uint32_t)((8 * gq + ((l & 15) >> 1)) * RSB + 8 * (l & 1));
+    const int* tail = gen + 64 * 4 * 3 * 128;
+    auto ld_b = [&](int rb, v4i& b0, v4i& b1, int& kt) {
+        auto ld2 = [&](int ks, int ty) {
+            return *reinterpret_cast<const v2i*>(gen + ((rb * 4 + ks) * 3 + ty) * 128 + l * 2);
+        };
+        const v2i x0 = ld2(0, 0), x1 = ld2(1, 0), y0 = ld2(2, 1), y1 = ld2(3, 1);
+        b0 = v4i{x0.x, x0.y, x1.x, x1.y};
+        b1 = v4i{y0.x, y0.y, y1.x, y1.y};
+        kt = tail[16 * rb + tl];
+    };
+    auto rb_body = [&](int rb, const v4i& b0, const v4i& b1, int kt) {
+#pragma unroll 1
+        for (int st = 0; st < 8; st++) {
+            v4u o0 = {acc + st, acc ^ st, acc + rb, acc}, o1 = {acc ^ rb, acc + 7, acc, acc ^ st};
+            if constexpr (MATH) {
+                v4i a4[4][3];
+#pragma unroll
+                for (int T = 0; T < 4; T++) {
+                    auto rd = [&](int ks) {
+                        auto* pa = (__attribute__((address_space(3))) v2i*)(
+                            ldsa + abase + 32 * ks * RSB + (4 * st + T) * 16);
+                        return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
+                    };
+                    const v2i p0 = rd(0), p1 = rd(1), p2 = rd(2), p3 = rd(3);
+                    const v4i h{p0.x, p0.y, p1.x, p1.y}, lo{p2.x, p2.y, p3.x, p3.y};
+                    a4[T][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(h, b0, v4i{0, 0, 0, 0}, 0, 0, 0);
+                    a4[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo, b1, v4i{kt, kt, kt, kt}, 0, 0, 0);
+                    a4[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(h, b1, v4i{0, 0, 0, 0}, 0, 0, 0);
+                    a4[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(lo, b0, a4[T][2], 0, 0, 0);
+                }
+                epilogue(a4, o0, o1);
+            }
+            const uint32_t rowb = (16 * rb + tl) * P * 2 + tile * TW * 2 + 128 * st + 16 * gq;
+            __builtin_amdgcn_raw_buffer_store_b128(o0, ro, rowb, 0, AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(o1, ro, rowb + 64, 0, AUX);
+        }
+    };
+    v4i bA0, bA1, bB0, bB1;
+    int ktA, ktB;
+    ld_b(w, bA0, bA1, ktA);
+    constexpr int NRB = 64 / NW;
+#pragma unroll 1
+    for (int jj = 0; jj < NRB; jj += 2) {
+        const int rb = w + NW * jj;
+        ld_b(rb + NW, bB0, bB1, ktB);
+        rb_body(rb, bA0, bA1, ktA);
+        ld_b(jj + 2 < NRB ? rb + 2 * NW : rb + NW, bA0, bA1, ktA);
+        rb_body(rb + NW, bB0, bB1, ktB);
+    }
+}
+
 template <typename F>
 float timeit(F f, int reps)
 {
@@ -369,9 +465,27 @@ int main(int argc, char** argv)
     CHECK(hipMalloc(&a, ab));
     CHECK(hipMalloc(&b, bb));
     CHECK(hipMalloc(&gen, gb));
-    CHECK(hipMemset(a, 1, ab));
     CHECK(hipMemset(b, 2, bb));
-    CHECK(hipMemset(gen, 0, gb));
+    // random data and operand tiles (argv[2] = "zero": the trivial fills;
+    // MFMAs on random operands draw more power and clock lower)
+    const bool zero = argc > 2 && argv[2][0] == 'z';
+    {
+        std::vector<uint32_t> h(ab / 4);
+        uint64_t x = 0x9E3779B97F4A7C15ull;
+        for (auto& v : h) {
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            v = zero ? 0x01010101u : static_cast<uint32_t>(x);
+        }
+        CHECK(hipMemcpy(a, h.data(), ab, hipMemcpyHostToDevice));
+        std::vector<uint32_t> hg(gb / 4);
+        for (size_t i = 0; i < hg.size(); i++) {
+            x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+            // operand bytes in [-128, 127]; the tail (kt, rowmap) small
+            hg[i] = zero ? 0u : i < 64 * 4 * 3 * 128 ? static_cast<uint32_t>(x) : static_cast<uint32_t>(x & 1023);
+        }
+        CHECK(hipMemcpy(gen, hg.data(), gb, hipMemcpyHostToDevice));
+    }
+    printf("data: %s\n", zero ? "trivial fills" : "random");
     const double eb = ab + bb;
     const int tiles = P / TW;
 #define RUN(LV, RS)                                                                        \
@@ -390,8 +504,26 @@ int main(int argc, char** argv)
         CHECK(hipGetLastError());                                                          \
         printf("cfg3 A-stationary epi%d  %7.3f ms %7.1f GB/s\n", EPI, ms, eb / ms / 1e6);  \
     }
+    constexpr int LDSH = IMG + 2048 + 16;
+#define RUNH(NW, MATH, AUX)                                                                \
+    {                                                                                      \
+        CHECK(hipFuncSetAttribute((const void*)enc_h<NW, MATH, AUX>,                      \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDSH));      \
+        float ms = timeit([&] { enc_h<NW, MATH, AUX><<<tiles * S, 64 * NW, LDSH>>>(a, b, gen, tiles); }, \
+                          reps);                                                           \
+        CHECK(hipGetLastError());                                                          \
+        printf("cfg3 half-line NW%d math%d aux%2d %7.3f ms %7.1f GB/s\n", NW, MATH, AUX, ms, \
+               eb / ms / 1e6);                                                             \
+    }
     for (int rep = 0; rep < 2; rep++) {
         printf("--- rep %d\n", rep);
+        RUNH(4, false, 0)
+        RUNH(4, false, 18)
+        RUNH(8, false, 0)
+        RUNH(8, false, 18)
+        RUNH(8, true, 0)
+        RUNH(8, true, 18)
+        RUNH(4, true, 0)
         RUN(0, 1)
         RUN(1, 1)
         RUN(2, 1)
