@@ -1576,6 +1576,232 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
 }
 
 // ---------------------------------------------------------------------------
+// Tall-generator encode at KS = 4 (33 <= k <= 64 and at least 64 output rows:
+// cfg3's 1024 x 64 generator).  matrix_mfma_kernel<4, 8, 4, true>'s geometry
+// and arithmetic -- a block of 4 waves stages 512 columns of the stripe's k
+// data rows as the byte-plane image, wave wv walks row blocks wv, wv + 4, ...
+// over all 8 super tiles, each 16 x 64 output tile transposed through the
+// wave's LDS tile into whole-line stores -- without what an encode never
+// meets: no input marks (no route tables, bucket scans, per-mark epilogue
+// loop or slow-tile list), no received ids, one source region.  Its OOR
+// outputs (value 65536) go to an LDS list recorded at the end of the block:
+// recording one in the epilogue (a returning global atomic) waited for every
+// store the wave had in flight.  A row block's operands come one row block
+// ahead; the super-tile loop stays plain (the pipelined pair loop measured
+// no gain).  The probe ladder of tools/membw7.hip (profiles/r5_ab_notes.txt)
+// puts this structure at the store shape's time.
+// ---------------------------------------------------------------------------
+template <int NST, int NW>
+__global__ __launch_bounds__(64 * NW) void gen_mfma_kernel(MatArgs a)
+{
+    constexpr int KS = 4;
+    using G = MfmaTile<KS, NST, NW>;
+    constexpr int NCOL = G::kCols, KH = G::kRows, RSB = G::kPitch;
+    constexpr int CPL = G::kCpl, RG = G::kRg;
+    static_assert(G::kTpr % 64 == 0, "row groups are wave-uniform");
+    extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
+    uint8_t* img = qi_lds;
+    int* s_i = reinterpret_cast<int*>(qi_lds + G::kImg);
+    uint32_t* s_col = reinterpret_cast<uint32_t*>(s_i + kMaxTileOor);
+    int* s_cnt = reinterpret_cast<int*>(s_col + kMaxTileOor);
+    const MatLayout L = a.L;
+    const Oor out_oor = a.out_oor;
+    const bool rec = out_oor.counts != nullptr;
+
+    int s, tile;
+    block_map(blockIdx.x, a.tiles, s, tile);
+    const int kin = L.kin;
+    const long long col0 = static_cast<long long>(tile) * NCOL;
+    const uint32_t cl = (RG == 1 ? threadIdx.x : threadIdx.x % G::kTpr) * CPL;
+    const int rg = RG == 1 ? 0 : static_cast<int>(threadIdx.x / G::kTpr);
+    const uint32_t voff = static_cast<uint32_t>((col0 + cl) * 2);
+    const int32_t* M = a.mat + s * a.ms;
+    const Region<true> g0(a.src.base0 + s * a.src.ss0, a.ext.e0);
+    const Region<true> go(a.dst.base + s * a.dst.ss, a.ext.eo);
+    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int g = l >> 4, q = (l & 15) >> 1, p = l & 1, tl = l & 15;
+    const int RB = L.RB();
+    const int32_t* mf = M + L.mf();
+    const int32_t* kmf = M + L.kmf();
+    const int32_t* rscale = M + L.rscale_mf();
+    const int32_t* __restrict__ rowmap = a.rowmap;
+
+    // a row block's operands: [a|0] over the h' K-steps (b0) and [0|b] over
+    // the l' K-steps (b1), as x64 pairs; [b|a] is b1 over the h' half and b0
+    // over the l' half, lane for lane (see matrix_mfma_kernel's load_ops)
+    struct Ops {
+        qi_v4i b0, b1;
+        int32_t kt, rs, pr[3];
+    };
+    auto load_ops = [&](int rb, Ops& o) {
+        auto ld2 = [&](int ks, int ty) {
+            return *reinterpret_cast<const qi_v2i*>(mf + ((rb * KS + ks) * 3 + ty) * 128 + l * 2);
+        };
+        const qi_v2i x0 = ld2(0, 0), x1 = ld2(1, 0), y0 = ld2(2, 1), y1 = ld2(3, 1);
+        o.b0 = qi_v4i{x0.x, x0.y, x1.x, x1.y};
+        o.b1 = qi_v4i{y0.x, y0.y, y1.x, y1.y};
+        // unconditional loads of a clamped row, selected after (an
+        // exec-masked load leaves the vmcnt count unknown to the compiler)
+        const int t = 16 * rb + tl, tc = t < L.R ? t : L.R - 1;
+        const int32_t k0 = kmf[tc], r0 = rscale[tc];
+        o.kt = t < L.R ? k0 : 0;
+        o.rs = t < L.R ? r0 : 1;
+        o.pr[0] = rowmap[tc];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int ot = 16 * rb + 8 * h + (l >> 3);
+            o.pr[1 + h] = rowmap[ot < L.R ? ot : L.R - 1];
+        }
+    };
+    const int rlast = RB - 1;
+    Ops oA, oB;
+    load_ops(min(wv, rlast), oA);
+
+    // stage the tile: this thread's CPL columns of every RG-th data row (rows
+    // past kin: a clamped row, their operand bytes are 0), all loads first
+    uint32_t w[KH / RG][CPL / 2];
+    {
+        const uint32_t rsb = static_cast<uint32_t>(a.src.rs0 * 2);
+#pragma unroll
+        for (int r = 0; r < KH / RG; r++) {
+            const int i = r * RG + rg;
+            ld_dw<CPL / 2, true, kAuxLd>(g0, static_cast<uint32_t>(i < kin ? i : kin - 1) * rsb,
+                                         voff, w[r]);
+        }
+    }
+    const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) + 4 * ((cl % 64) / 16) + cl % 4;
+#pragma unroll
+    for (int r = 0; r < KH / RG; r++) {
+        const int i = r * RG + rg;
+        if constexpr (CPL == 4) {
+            const uint32_t hi =
+                __builtin_amdgcn_perm(w[r][1], w[r][0], 0x07050301u) ^ 0x80808080u;
+            const uint32_t lo =
+                __builtin_amdgcn_perm(w[r][1], w[r][0], 0x06040200u) ^ 0x80808080u;
+            *reinterpret_cast<uint32_t*>(img + i * RSB + lpos) = hi;
+            *reinterpret_cast<uint32_t*>(img + (KH + i) * RSB + lpos) = lo;
+        } else {
+            const uint32_t hi = __builtin_amdgcn_perm(0u, w[r][0], 0x0c0c0301u) ^ 0x8080u;
+            const uint32_t lo = __builtin_amdgcn_perm(0u, w[r][0], 0x0c0c0200u) ^ 0x8080u;
+            *reinterpret_cast<uint16_t*>(img + i * RSB + lpos) = static_cast<uint16_t>(hi);
+            *reinterpret_cast<uint16_t*>(img + (KH + i) * RSB + lpos) = static_cast<uint16_t>(lo);
+        }
+    }
+    if (threadIdx.x == 0)
+        *s_cnt = 0;
+    __syncthreads();
+
+    const uint32_t ors = static_cast<uint32_t>(a.dst.rs * 2);
+    auto* lds = (__attribute__((address_space(3))) uint8_t*)img;
+    const uint32_t abase = static_cast<uint32_t>((8 * g + q) * RSB + 8 * p);
+    uint8_t* stg = qi_lds + G::kLds + wv * G::kStage;
+
+    auto rb_body = [&](int rb, const Ops& o) {
+        const int t = 16 * rb + tl;
+        const bool trow = t < L.R;
+        const qi_v4i ktv{o.kt, o.kt, o.kt, o.kt};
+#pragma unroll 1
+        for (int st = 0; st < NST; st++) {
+            qi_v4i acc[4][3];
+#pragma unroll
+            for (int T = 0; T < 4; T++) {
+                auto rd = [&](int ks) {
+                    auto* pa = (__attribute__((address_space(3))) qi_v2i*)(
+                        lds + abase + 32 * ks * RSB + (4 * st + T) * 16);
+                    return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
+                };
+                const qi_v2i h0 = rd(0), h1 = rd(1), l0 = rd(2), l1 = rd(3);
+                const qi_v4i ah{h0.x, h0.y, h1.x, h1.y}, al{l0.x, l0.y, l1.x, l1.y};
+                acc[T][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, o.b0, qi_v4i{0, 0, 0, 0},
+                                                                  0, 0, 0);
+                acc[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, o.b1, ktv, 0, 0, 0);
+                acc[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, o.b1, qi_v4i{0, 0, 0, 0},
+                                                                  0, 0, 0);
+                acc[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, o.b0, acc[T][2], 0, 0, 0);
+            }
+            // lane (g, t) holds row t, columns cb .. cb + 15 (the image's
+            // column order): y = 256 D2 + D1 - D0, kt in D1
+            const long long cb = col0 + 64 * st + 16 * g;
+            int32_t y[16];
+#pragma unroll
+            for (int T = 0; T < 4; T++)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    y[4 * T + j] = fold(fold((acc[T][2][j] << 8) + acc[T][1][j] - acc[T][0][j]));
+            if (__builtin_amdgcn_ballot_w64(o.rs != 1)) {
+#pragma unroll
+                for (int c = 0; c < 16; c++)
+                    y[c] = fold(fold(mul_rs(y[c], o.rs)));
+            }
+            uint32_t bad = 0;
+#pragma unroll
+            for (int c = 0; c < 16; c++)
+                bad |= static_cast<uint32_t>(y[c]);
+            if (__builtin_expect(__builtin_amdgcn_ballot_w64((bad >> 16) != 0) != 0, 0)) {
+#pragma unroll
+                for (int c = 0; c < 16; c++) {
+                    if (static_cast<uint32_t>(y[c]) > 65535u) {
+                        if (rec && trow) {
+                            // LDS atomic: no wait on the stores in flight
+                            const int e = atomicAdd(s_cnt, 1);
+                            if (e < kMaxTileOor) {
+                                s_i[e] = o.pr[0];
+                                s_col[e] = static_cast<uint32_t>(cb + c);
+                            } else {
+                                record_oor(out_oor, s, o.pr[0], cb + c);
+                            }
+                        }
+                        y[c] = 0;  // 65536 (or its alias -1) is stored as 0
+                    }
+                }
+            }
+            qi_v4u o0, o1;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                o0[c] = pack_lo(static_cast<uint32_t>(y[2 * c]), static_cast<uint32_t>(y[2 * c + 1]));
+                o1[c] = pack_lo(static_cast<uint32_t>(y[8 + 2 * c]),
+                                static_cast<uint32_t>(y[8 + 2 * c + 1]));
+            }
+            *reinterpret_cast<qi_v4u*>(stg + tl * G::kStagePitch + 32 * g) = o0;
+            *reinterpret_cast<qi_v4u*>(stg + tl * G::kStagePitch + 32 * g + 16) = o1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int orow = 8 * h + (l >> 3), c = l & 7;
+                const qi_v4u v =
+                    *reinterpret_cast<const qi_v4u*>(stg + orow * G::kStagePitch + 16 * c);
+                // rows >= R: an offset past the extent (< 2^31), dropped
+                const int ot = 16 * rb + orow;
+                const uint32_t vo =
+                    ot < L.R ? static_cast<uint32_t>(o.pr[1 + h]) * ors +
+                                   static_cast<uint32_t>((col0 + 64 * st + 8 * c) * 2)
+                             : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(v, go.r, static_cast<int>(vo), 0, kAuxStMf);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+    };
+    // row blocks in ping-pong over two operand sets, each prefetched one row
+    // block ahead and unconditional (a clamped row block past the end)
+    for (int rb = wv; rb < RB; rb += 2 * NW) {
+        load_ops(min(rb + NW, rlast), oB);
+        rb_body(rb, oA);
+        if (rb + NW >= RB)
+            break;
+        load_ops(min(rb + 2 * NW, rlast), oA);
+        rb_body(rb + NW, oB);
+    }
+    // the block's OOR outputs into their buckets
+    __syncthreads();
+    const int n = min(*s_cnt, kMaxTileOor);
+    for (int e = threadIdx.x; e < n; e += 64 * NW)
+        record_oor(out_oor, s, s_i[e], s_col[e]);
+}
+
+// ---------------------------------------------------------------------------
 // Operand-stationary matrix-core kernel (KS = 4, 8, 16: 32 < kin <= 256; the
 // decodes of k = 33 .. 256 and the generators of those codes).
 //
@@ -2250,6 +2476,36 @@ static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+#ifndef QI_GEN_MFMA
+#define QI_GEN_MFMA 1
+#endif
+static constexpr bool kGenMfma = QI_GEN_MFMA;
+
+static int gen_launch(MatArgs a, long long wfull, int S, hipStream_t st)
+{
+    constexpr int NST = 8, NW = 4;
+    using G = MfmaTile<4, NST, NW>;
+    const long long t = wfull / G::kCols;
+    if (t <= 0 || t * S > 0x7fffffffLL)
+        return -1;
+    a.tiles = static_cast<int>(t);
+    static std::atomic<uint64_t> attr_done{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return -2;
+    const uint64_t bit = dev < 64 ? 1ull << dev : 0;
+    if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gen_mfma_kernel<NST, NW>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(G::kLdsStaged)) != hipSuccess)
+            return -2;
+        attr_done.fetch_or(bit, std::memory_order_release);
+    }
+    hipLaunchKernelGGL((gen_mfma_kernel<NST, NW>), dim3(t * S), dim3(G::kThreads),
+                       G::kLdsStaged, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // Block geometry by matrix shape (kRouteTile = 1024 must be a multiple of
 // the block width):
 //  - short matrices (RB < 4: decodes, k x k): 4 waves, each on its own super
@@ -2368,6 +2624,13 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
         (void)RB;
         return mfma_launch<KS, 4, 4, true>(a, wfull, S, st);
     } else {
+        if constexpr (KS == 4) {
+            // a tall generator over one source region (every encode):
+            // the lean generator kernel
+            if (RB >= 4 && kGenMfma && !a.in_oor.counts && !a.route && !a.ids &&
+                !a.src.base1)
+                return gen_launch(a, wfull, S, st);
+        }
         if (RB >= 4)
             return mfma_launch<KS, NSTG, KS == 4 ? kEnc4Nw : 4, true>(a, wfull, S, st);
         return mfma_launch<KS, NSTS, 4, false>(a, wfull, S, st);
@@ -2478,6 +2741,8 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
         if (og.wr)
             r = "matrix_os_kernel<" + std::to_string(KS) + ", " + std::to_string(og.wr) + ", " +
                 std::to_string(og.rpw) + ", " + tf(two) + ">";
+        else if (KS == 4 && RB >= 4 && kGenMfma && !in_oor && !two)
+            r = "gen_mfma_kernel<8, 4>";  // (an encode: no ids, no input marks)
         else
             r = "matrix_mfma_kernel<" + std::to_string(KS) + ", " + std::to_string(nst) + ", " +
                 std::to_string(nw) + ", " + tf(rsplit) + ">";
