@@ -55,6 +55,9 @@ CONFIGS = {
     "k300": (300, 212, 65536, 32),   # n = 512: the matrix cores at KS = 20
     "k384": (384, 128, 65536, 32),   # n = 512: the largest matrix-path k
     "k1000": (1000, 24, 65536, 16),  # n = 1024, len_2k = 2048: NTT engine
+    # general decode at k > 384 with n - k > 64 (no erasure solve): the
+    # reference's INTT_n -> NTT_2k -> x C -> INTT_2k pipeline on the engine
+    "k600": (600, 1400, 65536, 16),  # n = 2048, len_2k = 2048
     # cfg3's code at 64 KiB packets (the same bytes per step as cfg3)
     "cfg3p64": (64, 960, 65536, 64),
 }

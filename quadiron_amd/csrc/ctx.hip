@@ -210,10 +210,7 @@ constexpr int kPackNj = kMatMaxKin / 4;
 // 64 rows = 4 row blocks per packing pass at 16 lanes per row (32 rows at 32
 // lanes: twice the passes and barriers for the same work; contexts k256
 // 120 -> 114 us, k300 179 -> 161 us, k384 219 -> 206 us)
-#ifndef QI_CTX_CHUNK
-#define QI_CTX_CHUNK 64
-#endif
-constexpr int kCtxChunk = QI_CTX_CHUNK;
+constexpr int kCtxChunk = 64;
 constexpr int kCtxLdsCap = 160 * 1024;
 
 // One pass: NT / LPR rows from row block rb0 on (LPR lanes per row); row

@@ -586,6 +586,11 @@ __device__ __forceinline__ void push_slow_tile(const SlowList& sl, int s, long l
 // is emptied afterwards (a context can serve several decodes).
 constexpr int kRedoCols = 64;
 
+// A block checks the lists of kRedoSpan stripes at once (one lane each) and
+// walks only the stripes holding slow tiles: with one block per stripe the
+// launch cost 4-5 us even with every list empty (cfg3 decode).
+constexpr int kRedoSpan = 64;
+
 __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_stripes)
 {
     __shared__ uint16_t xs[kMatMaxKin * kRedoCols];  // [input i][column]
@@ -597,11 +602,27 @@ __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_st
     const RowDst dst = a.dst;
     const Oor in = a.in_oor;
     const int tid = threadIdx.x, c = tid & 63, wv = tid >> 6;
-    for (int s = blockIdx.x; s < n_stripes; s += gridDim.x) {
+    // this block's stripes with a non-empty list (wave 0, one lane each;
+    // broadcast to the block through LDS)
+    __shared__ uint64_t todo;
+    const int s0 = blockIdx.x * kRedoSpan;
+    if (wv == 0) {
+        const int sl = s0 + c;
+        const uint32_t nl = sl < n_stripes
+                                ? __hip_atomic_load(a.slow.base + sl * a.slow.stride,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : 0u;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(nl != 0);
+        if (c == 0)
+            todo = m;
+    }
+    __syncthreads();
+    uint64_t pend = todo;
+    while (pend) {
+        const int s = s0 + __builtin_ctzll(pend);  // block-uniform
+        pend &= pend - 1;
         uint32_t* l = a.slow.base + s * a.slow.stride;
-        const uint32_t n = __hip_atomic_load(l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n == 0)
-            continue;  // block-uniform
+        const uint32_t n = *l;
         const int32_t* M = a.mat + s * a.ms;
         const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
         const int32_t* rscale = M + L.rscale();
@@ -1045,26 +1066,10 @@ __global__ __launch_bounds__(kBlock) void matrix_kernel(MatArgs a)
 // matrix_kernel.
 // ---------------------------------------------------------------------------
 typedef int qi_v4i __attribute__((ext_vector_type(4)));
-// the KS = 4 super-tile loop in pairs, the next tile's MFMAs interleaved
-// with this one's epilogue (cfg3 encode 1.078 -> 1.063 ms; at KS = 2 the
-// second accumulator set cost occupancy: k32 decode 0.83 -> 0.99 ms)
-static constexpr bool kMmPipe = true;
-// the tall KS = 4 generators (cfg3's 1024 x 64 encode): super tiles per
-// block and whether the pipelined pair loop runs (A/B knobs).  Smaller
-// blocks buy occupancy (125 VGPRs without the pair loop) and lose: cfg3
-// encode 1.05 ms at 8 super tiles + pairs (2 waves/SIMD), 1.06 without the
-// pairs, 1.16 at 4 (3 blocks per CU), 1.37 at 2 (gpurun_out ab_geo)
-#ifndef QI_ENC4_NST
-#define QI_ENC4_NST 8
-#endif
-#ifndef QI_ENC4_PIPE
-#define QI_ENC4_PIPE 1
-#endif
-#ifndef QI_ENC4_NW
-#define QI_ENC4_NW 4
-#endif
-static constexpr int kEnc4Nst = QI_ENC4_NST;
-static constexpr int kEnc4Nw = QI_ENC4_NW;
+// (The tall KS = 4 generators -- cfg3's 1024 x 64 -- run gen_mfma_kernel;
+// this kernel's super-tile loop is plain.  Round 3's pipelined pair loop for
+// them, the next tile's MFMAs interleaved with this one's epilogue, measured
+// no gain against a plain loop in round 5: profiles/r5_ab_notes.txt.)
 typedef int qi_v2i __attribute__((ext_vector_type(2)));
 typedef unsigned int qi_v4u __attribute__((ext_vector_type(4)));
 
@@ -1502,52 +1507,13 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             __builtin_amdgcn_wave_barrier();
         };
         auto st_of = [&](int st) { return rsplit ? st : wv * nst + st; };
-        if constexpr (kMmPipe && QI_ENC4_PIPE && KS == 4 && nst >= 2 && nst % 2 == 0) {
-            // software pipeline over super-tile pairs: the MFMAs of tile
-            // st + 1 are issued between the element math of tile st (two
-            // accumulator sets), interleaved by sched_group_barrier so the
-            // matrix pipe runs under the epilogue's VALU instead of after it
-            constexpr int NMF = 4 * (KS == 2 ? 3 : 3 * KS / 2 - KS / 2);  // MFMAs per tile
-            constexpr int NDS = 4 * KS;                                   // A reads per tile
-            constexpr int VPM = (KS >= 16 ? 80 : 64) / NMF;               // VALU per MFMA
-            qi_v4i a0[4][3], a1[4][3];
-            auto interleave = [&]() {
-                __builtin_amdgcn_sched_group_barrier(0x100, NDS, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-#pragma unroll
-                for (int i = 0; i < NMF; i++) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
-                }
-            };
-            auto pair = [&](int st, auto last_c) {
-                constexpr bool last = decltype(last_c)::value;
-                int32_t y[16];
-                tile_mfma(st_of(st + 1), a1);
-                tile_y(a0, y);
-                interleave();
-                tile_fin(st_of(st), y);
-                if constexpr (!last)
-                    tile_mfma(st_of(st + 2), a0);
-                tile_y(a1, y);
-                if constexpr (!last)
-                    interleave();
-                tile_fin(st_of(st + 1), y);
-            };
-            tile_mfma(st_of(0), a0);
 #pragma unroll 1
-            for (int st = 0; st < nst - 2; st += 2)
-                pair(st, std::false_type{});
-            pair(nst - 2, std::true_type{});
-        } else {
-#pragma unroll 1
-            for (int st = 0; st < nst; st++) {
-                qi_v4i acc[4][3];
-                int32_t y[16];
-                tile_mfma(st_of(st), acc);
-                tile_y(acc, y);
-                tile_fin(st_of(st), y);
-            }
+        for (int st = 0; st < nst; st++) {
+            qi_v4i acc[4][3];
+            int32_t y[16];
+            tile_mfma(st_of(st), acc);
+            tile_y(acc, y);
+            tile_fin(st_of(st), y);
         }
     };
     // Row blocks in ping-pong over two operand buffers, each prefetch one row
@@ -1989,14 +1955,14 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             off0[r] = static_cast<uint32_t>(id * src.rs0 * 2) + lane;
         }
     }
-    // DEEP (KS = 4, the short decodes): two tiles of rows in flight per
-    // block (two register sets) -- with one, a CU kept ~32 KB of loads in
-    // flight and the cfg3 decode was bound by the load latency
-#ifndef QI_OS_DEEP
-#define QI_OS_DEEP 1
-#endif
-    constexpr bool DEEP = QI_OS_DEEP && KS == 4;
-    uint32_t w[RPT][2], w2[DEEP ? RPT : 1][2];
+    // DEEP (KS = 4, the short decodes): ND tiles of rows in flight per
+    // block (a ring of ND register sets, 8 VGPRs each) -- with one, a CU
+    // kept ~32 KB of loads in flight and the cfg3 decode was bound by the
+    // load latency; three measured the same as two, four slower (125 / 133
+    // VGPRs: cfg3 decode 0.143 / 0.168 ms, profiles/r5_ab_notes.txt)
+    constexpr int ND = KS == 4 ? 2 : 1;
+    constexpr bool DEEP = ND >= 2;
+    uint32_t w[RPT][2], wring[DEEP ? ND : 1][DEEP ? RPT : 1][2];
     // rows of `tile` into wr; an invalid tile (past the block's range) loads
     // from past the buffer's extent (no memory access, zeros), so the number
     // of loads in flight is the same on every path
@@ -2208,43 +2174,50 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         return;
     auto img = [&](int b) { return qi_lds + b * O::kImg; };
     if constexpr (DEEP) {
-        issue_rows_to(t0, true, w);
-        issue_rows_to(t0 + 1, t0 + 1 < t1, w2);
-        write_rows_from(img(0), w);
+        // tiles t0 .. t0 + ND - 1 in flight, the first one into image 0
+#pragma unroll
+        for (int d = 0; d < ND; d++)
+            issue_rows_to(t0 + d, t0 + d < t1, wring[d]);
+        write_rows_from(img(0), wring[0]);
         int nl[2];
         nl[0] = stage_marks(t0, 0);
         nl[1] = 0;
         __syncthreads();
-        // tile's rows are in image b; wnext holds tile + 1's (in flight),
-        // wfree is free: it takes tile + 2's
-        auto body = [&](int tile, auto& wnext, auto& wfree) {
+        // tile's rows are in image b; set J (tile's, already written) takes
+        // tile + ND's, set J + 1 holds tile + 1's (in flight)
+        auto body = [&](int tile, auto jc) {
+            constexpr int J = decltype(jc)::value;
             const int b = (tile - t0) & 1;
             const bool more = tile + 1 < t1;  // block-uniform
-            issue_rows_to(tile + 2, tile + 2 < t1, wfree);
+            issue_rows_to(tile + ND, tile + ND < t1, wring[J]);
             const long long col0 = static_cast<long long>(tile) * NCOL + 64 * st;
             auto none = [] {};
-            [&]<int... J>(std::integer_sequence<int, J...>) {
-                ((act[J] ? compute(img(b), col0, nl[b], s_i(b), s_col(b),
-                                   std::integral_constant<int, J>{}, none)
+            [&]<int... R>(std::integer_sequence<int, R...>) {
+                ((act[R] ? compute(img(b), col0, nl[b], s_i(b), s_col(b),
+                                   std::integral_constant<int, R>{}, none)
                          : idle_stores()),
                  ...);
             }(std::make_integer_sequence<int, RPW>{});
-            // unconditional, so every path waits for wnext's loads here (a
-            // skipped write left them pending on one path, and the compiler
-            // then drained vmcnt(0) before reusing the registers); past the
-            // last tile it writes the invalid tile's zeros into an image no
-            // wave reads again
-            write_rows_from(img(b ^ 1), wnext);
+            // unconditional, so every path waits for the next set's loads
+            // here (a skipped write left them pending on one path, and the
+            // compiler then drained vmcnt(0) before reusing the registers);
+            // past the last tile it writes the invalid tile's zeros into an
+            // image no wave reads again
+            write_rows_from(img(b ^ 1), wring[(J + 1) % ND]);
             if (more)
                 nl[b ^ 1] = stage_marks(tile + 1, b ^ 1);
             __syncthreads();
         };
 #pragma unroll 1
-        for (int tile = t0; tile < t1; tile += 2) {
-            body(tile, w2, w);
-            if (tile + 1 >= t1)
+        for (int tile = t0; tile < t1; tile += ND) {
+            bool done = false;
+            [&]<int... J>(std::integer_sequence<int, J...>) {
+                ((done = done || tile + J >= t1, done ? void() : body(tile + J,
+                                                                     std::integral_constant<int, J>{})),
+                 ...);
+            }(std::make_integer_sequence<int, ND>{});
+            if (done)
                 break;
-            body(tile + 1, w, w2);
         }
         return;
     }
@@ -2476,10 +2449,6 @@ static int mfma_launch(MatArgs a, long long wfull, int S, hipStream_t st)
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-#ifndef QI_GEN_MFMA
-#define QI_GEN_MFMA 1
-#endif
-static constexpr bool kGenMfma = QI_GEN_MFMA;
 
 static int gen_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 {
@@ -2606,7 +2575,6 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
             return os_launch<KS, 8, 1>(a, wfull, S, st);
     }
     constexpr int NSTS = KS == 1 ? 16 : 8;
-    constexpr int NSTG = KS == 4 ? kEnc4Nst : NSTS;  // tall generators
     const int RB = a.L.RB();
     if constexpr (KS > 16) {
         return -1;  // only the operand-stationary kernel takes kin > 256
@@ -2627,12 +2595,12 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
         if constexpr (KS == 4) {
             // a tall generator over one source region (every encode):
             // the lean generator kernel
-            if (RB >= 4 && kGenMfma && !a.in_oor.counts && !a.route && !a.ids &&
+            if (RB >= 4 && !a.in_oor.counts && !a.route && !a.ids &&
                 !a.src.base1)
                 return gen_launch(a, wfull, S, st);
         }
         if (RB >= 4)
-            return mfma_launch<KS, NSTG, KS == 4 ? kEnc4Nw : 4, true>(a, wfull, S, st);
+            return mfma_launch<KS, NSTS, 4, true>(a, wfull, S, st);
         return mfma_launch<KS, NSTS, 4, false>(a, wfull, S, st);
     }
 }
@@ -2726,10 +2694,6 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
         const int RB = L.RB();
         int nst = KS == 1 ? 16 : 8, nw = 4;
         bool rsplit = RB >= 4;
-        if (KS == 4 && rsplit) {
-            nst = kEnc4Nst;
-            nw = kEnc4Nw;
-        }
         if (KS == 16) {
             nst = 1;
             rsplit = true;
@@ -2741,7 +2705,7 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
         if (og.wr)
             r = "matrix_os_kernel<" + std::to_string(KS) + ", " + std::to_string(og.wr) + ", " +
                 std::to_string(og.rpw) + ", " + tf(two) + ">";
-        else if (KS == 4 && RB >= 4 && kGenMfma && !in_oor && !two)
+        else if (KS == 4 && RB >= 4 && !in_oor && !two)
             r = "gen_mfma_kernel<8, 4>";  // (an encode: no ids, no input marks)
         else
             r = "matrix_mfma_kernel<" + std::to_string(KS) + ", " + std::to_string(nst) + ", " +
@@ -2783,7 +2747,7 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
     if (rc || !in_oor)
         return rc;
     // tiles with more marks than the kernels' LDS list: see push_slow_tile
-    const int grid = S < 1024 ? S : 1024;
+    const int grid = (S + kRedoSpan - 1) / kRedoSpan;
     hipLaunchKernelGGL(matrix_redo_kernel, dim3(grid), dim3(kBlock), 0, st, a, S);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

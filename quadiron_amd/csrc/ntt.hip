@@ -1768,12 +1768,8 @@ int lds_launch(const qi_plan* p, NttLdsArgs a, int S, hipStream_t st)
     // the non-systematic encode runs NTT_n alone and could take an n-row
     // image (wider tiles where len_2k > n); measured slower at k1000 (T = 16
     // instead of 8: encode 1.27-1.29 -> 1.33 ms, gpurun_out ab_route), so the
-    // image stays nmax rows (QI_ENC_NIMG=1: the n-row variant)
-#ifndef QI_ENC_NIMG
-#define QI_ENC_NIMG 0
-#endif
-    if (QI_ENC_NIMG && a.mode == kLdsEnc)
-        a.nmax = p->n;
+    // image stays nmax rows (the n-row variant measured 1.31 vs 1.25 ms
+    // after the padded rows, round 4)
     bool twg;
     a.lgT = lds_geom(p, a.tw_words, &twg, a.nmax);
     if (a.lgT < 0)
@@ -1990,7 +1986,7 @@ std::string ntt_kernel_names(const qi_plan* p, bool decode)
     int lo, hi;
     lds_table_range(p, mode, &lo, &hi);
     bool twg;
-    (void)lds_geom(p, hi - lo, &twg, QI_ENC_NIMG && mode == kLdsEnc ? p->n : p->nmax);
+    (void)lds_geom(p, hi - lo, &twg, p->nmax);
     return std::string(decode ? "ntt_ctx_kernel + " : "") +
            (twg ? "ntt_lds_kernel<true>" : "ntt_lds_kernel<false>");
 }

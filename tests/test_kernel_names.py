@@ -28,7 +28,7 @@ def _names(kernels):
 @pytest.mark.parametrize("cfg,sys_", [
     ("cfg2", False), ("cfg2", True), ("cfg3", False), ("cfg1", False),
     ("k32", False), ("k128", False), ("k200", False), ("k256", False),
-    ("k300", False), ("k384", False), ("k1000", False),
+    ("k300", False), ("k384", False), ("k1000", False), ("k600", False),
 ])
 def test_reported_kernels_exist(cfg, sys_):
     import quadiron_amd as qa
