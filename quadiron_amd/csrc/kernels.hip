@@ -586,9 +586,94 @@ __device__ __forceinline__ void push_slow_tile(const SlowList& sl, int s, long l
 // is emptied afterwards (a context can serve several decodes).
 constexpr int kRedoCols = 64;
 
-// A block checks the lists of kRedoSpan stripes at once (one lane each) and
-// walks only the stripes holding slow tiles: with one block per stripe the
-// launch cost 4-5 us even with every list empty (cfg3 decode).
+// Recompute, from scratch, every column of stripe s's columns [t0c, t1c)
+// that holds a mark (all marks of the column restored, plain canonical
+// arithmetic) and store it again: NT threads, LDS scratch xs (kin x
+// kRedoCols u16), mk (kin x kRedoCols / 32 u32), colmk (kRedoCols / 32 u32).
+// The caller has waited for its own stores of these columns.
+template <int NT>
+__device__ void redo_columns(const MatArgs& a, int s, long long t0c, long long t1c,
+                             uint16_t* xs, uint32_t* mk, uint32_t* colmk)
+{
+    const MatLayout L = a.L;
+    const int kin = L.kin;
+    const RowSrc& src = a.src;
+    const RowDst& dst = a.dst;
+    const Oor& in = a.in_oor;
+    const int tid = threadIdx.x, c = tid & 63, wv = tid >> 6;
+    const int32_t* M = a.mat + s * a.ms;
+    const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
+    const int32_t* rscale = M + L.rscale();
+    const int32_t* mf = M + L.mf();
+    auto id_of = [&](int i) { return src.by_pos ? i : (sid ? sid[i] : i); };
+    for (long long c0 = t0c; c0 < t1c; c0 += kRedoCols) {
+        for (int j = tid; j < kin * (kRedoCols / 32); j += NT)
+            mk[j] = 0;
+        if (tid < kRedoCols / 32)
+            colmk[tid] = 0;
+        // the chunk's received symbols, one row of 64 per wave pass
+        for (int i = wv; i < kin; i += NT / 64) {
+            const int id = id_of(i);
+            const uint16_t* row = id < src.split
+                                      ? src.base0 + s * src.ss0 + id * src.rs0
+                                      : src.base1 + s * src.ss1 + (id - src.split) * src.rs1;
+            xs[i * kRedoCols + c] = c0 + c < t1c ? row[c0 + c] : 0;
+        }
+        __syncthreads();
+        // every mark of every received row inside the chunk
+        for (int i = tid; i < kin; i += NT) {
+            const int slot = (src.by_pos ? i : id_of(i)) - a.slot_base;
+            if (slot < 0)
+                continue;  // systematic data row: no marks
+            const long long bk = static_cast<long long>(s) * in.slots + slot;
+            const uint32_t cnt = min(in.counts[bk], static_cast<uint32_t>(in.cap));
+            for (uint32_t f = 0; f < cnt; f++) {
+                const long long w = in.entries[bk * in.cap + f];
+                if (w >= c0 && w < c0 + kRedoCols && w < t1c) {
+                    const int cc = static_cast<int>(w - c0);
+                    atomicOr(&mk[i * (kRedoCols / 32) + cc / 32], 1u << (cc % 32));
+                    atomicOr(&colmk[cc / 32], 1u << (cc % 32));
+                }
+            }
+        }
+        __syncthreads();
+        if ((colmk[c / 32] >> (c % 32)) & 1u) {
+            for (int t = wv; t < L.R; t += NT / 64) {
+                uint64_t acc = 0;
+                for (int j = 0; j < kin; j++) {
+                    const uint32_t x = (mk[j * (kRedoCols / 32) + c / 32] >> (c % 32)) & 1u
+                                           ? 65536u
+                                           : xs[j * kRedoCols + c];
+                    acc += static_cast<uint64_t>(mf_entry(L, mf, t, j)) * x;
+                }
+                uint32_t y = static_cast<uint32_t>(acc % 65537u);
+                const int32_t rs = rscale[t];
+                if (rs != 1)
+                    y = static_cast<uint32_t>(static_cast<uint64_t>(y) *
+                                              static_cast<uint32_t>(rs < 0 ? rs + kQ : rs) %
+                                              65537u);
+                dst.base[s * dst.ss + a.rowmap[t] * dst.rs + c0 + c] =
+                    static_cast<uint16_t>(y == 65536u ? 0u : y);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// A block's slow tiles (see push_slow_tile), redone by the block itself at
+// its end, after its waves' stores: the separate redo launch cost 4-5 us per
+// decode even with nothing to redo.  Waits for this wave's outstanding
+// memory operations (stores included), then the block barrier.
+__device__ __forceinline__ void drain_block_stores()
+{
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+    __syncthreads();
+}
+
+// The dot2 kernel's slow tiles (column tails, unaligned rows): kept in the
+// context's slow list and redone by this launch after it.  A block checks
+// the lists of kRedoSpan stripes at once (one lane each) and walks only the
+// stripes holding slow tiles.
 constexpr int kRedoSpan = 64;
 
 __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_stripes)
@@ -596,11 +681,6 @@ __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_st
     __shared__ uint16_t xs[kMatMaxKin * kRedoCols];  // [input i][column]
     __shared__ uint32_t mk[kMatMaxKin * (kRedoCols / 32)];
     __shared__ uint32_t colmk[kRedoCols / 32];
-    const MatLayout L = a.L;
-    const int kin = L.kin;
-    const RowSrc src = a.src;
-    const RowDst dst = a.dst;
-    const Oor in = a.in_oor;
     const int tid = threadIdx.x, c = tid & 63, wv = tid >> 6;
     // this block's stripes with a non-empty list (wave 0, one lane each;
     // broadcast to the block through LDS)
@@ -623,69 +703,12 @@ __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_st
         pend &= pend - 1;
         uint32_t* l = a.slow.base + s * a.slow.stride;
         const uint32_t n = *l;
-        const int32_t* M = a.mat + s * a.ms;
-        const int32_t* sid = a.ids ? a.ids + s * a.is : nullptr;
-        const int32_t* rscale = M + L.rscale();
-        const int32_t* mf = M + L.mf();
-        auto id_of = [&](int i) { return src.by_pos ? i : (sid ? sid[i] : i); };
         for (uint32_t e = 0; e < n; e++) {
             const uint32_t code = l[1 + e];
             const long long t0 = static_cast<long long>(code >> 3) * kSlowGrain;
             const long long t1 = min(t0 + (static_cast<long long>(kSlowGrain) << (code & 7)),
                                      a.words);
-            for (long long c0 = t0; c0 < t1; c0 += kRedoCols) {
-                for (int j = tid; j < kin * (kRedoCols / 32); j += kBlock)
-                    mk[j] = 0;
-                if (tid < kRedoCols / 32)
-                    colmk[tid] = 0;
-                // the chunk's received symbols, one row of 64 per wave pass
-                for (int i = wv; i < kin; i += kBlock / 64) {
-                    const int id = id_of(i);
-                    const uint16_t* row =
-                        id < src.split ? src.base0 + s * src.ss0 + id * src.rs0
-                                       : src.base1 + s * src.ss1 + (id - src.split) * src.rs1;
-                    xs[i * kRedoCols + c] = c0 + c < t1 ? row[c0 + c] : 0;
-                }
-                __syncthreads();
-                // every mark of every received row inside the chunk
-                for (int i = tid; i < kin; i += kBlock) {
-                    const int slot = (src.by_pos ? i : id_of(i)) - a.slot_base;
-                    if (slot < 0)
-                        continue;  // systematic data row: no marks
-                    const long long bk = static_cast<long long>(s) * in.slots + slot;
-                    const uint32_t cnt = min(in.counts[bk], static_cast<uint32_t>(in.cap));
-                    for (uint32_t f = 0; f < cnt; f++) {
-                        const long long w = in.entries[bk * in.cap + f];
-                        if (w >= c0 && w < c0 + kRedoCols && w < t1) {
-                            const int cc = static_cast<int>(w - c0);
-                            atomicOr(&mk[i * (kRedoCols / 32) + cc / 32], 1u << (cc % 32));
-                            atomicOr(&colmk[cc / 32], 1u << (cc % 32));
-                        }
-                    }
-                }
-                __syncthreads();
-                if ((colmk[c / 32] >> (c % 32)) & 1u) {
-                    for (int t = wv; t < L.R; t += kBlock / 64) {
-                        uint64_t acc = 0;
-                        for (int j = 0; j < kin; j++) {
-                            const uint32_t x =
-                                (mk[j * (kRedoCols / 32) + c / 32] >> (c % 32)) & 1u
-                                    ? 65536u
-                                    : xs[j * kRedoCols + c];
-                            acc += static_cast<uint64_t>(mf_entry(L, mf, t, j)) * x;
-                        }
-                        uint32_t y = static_cast<uint32_t>(acc % 65537u);
-                        const int32_t rs = rscale[t];
-                        if (rs != 1)
-                            y = static_cast<uint32_t>(
-                                static_cast<uint64_t>(y) *
-                                static_cast<uint32_t>(rs < 0 ? rs + kQ : rs) % 65537u);
-                        dst.base[s * dst.ss + a.rowmap[t] * dst.rs + c0 + c] =
-                            static_cast<uint16_t>(y == 65536u ? 0u : y);
-                    }
-                }
-                __syncthreads();
-            }
+            redo_columns<kBlock>(a, s, t0, t1, xs, mk, colmk);
         }
         __syncthreads();
         if (tid == 0)
@@ -1537,8 +1560,15 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
             rb_body(rb + rbs, bB, ktB, rsB, prB);
         }
     }
-    if (sc.slow && threadIdx.x == 0)  // rare: see matrix_redo_kernel
-        push_slow_tile(slow, s, col0, NCOL);
+    if (sc.slow) {
+        // rare (block-uniform): more marks than the LDS list held; this
+        // block redoes its columns once its stores are done, with the image
+        // as scratch (kin x 136 bytes <= the image)
+        drain_block_stores();
+        redo_columns<64 * NW>(a, s, col0, col1, reinterpret_cast<uint16_t*>(qi_lds),
+                              reinterpret_cast<uint32_t*>(qi_lds + kin * 2 * kRedoCols),
+                              reinterpret_cast<uint32_t*>(qi_lds + kin * (2 * kRedoCols + 8)));
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1882,6 +1912,11 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     }
     const int t0 = static_cast<int>(static_cast<long long>(cr) * TS / C);
     const int t1 = static_cast<int>(static_cast<long long>(cr + 1) * TS / C);
+    // one bit per tile of the block (<= kOsMaxTiles, os_launch), behind the
+    // other LDS sections; cleared before the first mark scan's barrier
+    uint32_t* slow_bits = reinterpret_cast<uint32_t*>(qi_lds + O::kLds);
+    for (int wd = tid; wd <= (t1 - t0 - 1) >> 5; wd += 512)
+        slow_bits[wd] = 0u;
 
     const int RB = L.RB();
     const int slot = wv % WR, st = wv / WR;  // row-block slot, super tile
@@ -2021,9 +2056,32 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         OorScan sc{in_oor, sid, src.by_pos, a.slot_base, kin, s, false};
         const int cnt = scan_tile_marks(sc, col0, col0 + NCOL, a.words, s_cnt(mb), s_i(mb),
                                         s_col(mb), a.err);
-        if (cnt > kMaxTileOor && tid == 0)  // rare: see matrix_redo_kernel
-            push_slow_tile(a.slow, s, col0, NCOL);
+        if (cnt > kMaxTileOor && tid == 0)  // rare: redone at the block's end
+            atomicOr(&slow_bits[(tile - t0) >> 5], 1u << ((tile - t0) & 31));
         return min(cnt, kMaxTileOor);
+    };
+    // the block's slow tiles (bits over [t0, t1)), redone by the block once
+    // its stores are done, with the images as scratch
+    auto finish = [&]() {
+        if (!marks_in)
+            return;
+        bool any = false;
+        for (int wd = 0; wd <= (t1 - t0 - 1) >> 5; wd++)
+            any |= slow_bits[wd] != 0u;
+        if (!any)
+            return;  // block-uniform
+        drain_block_stores();
+        for (int wd = 0; wd <= (t1 - t0 - 1) >> 5; wd++) {
+            uint32_t bits = slow_bits[wd];
+            while (bits) {
+                const int tile = t0 + 32 * wd + __builtin_ctz(bits);
+                bits &= bits - 1;
+                const long long c0 = static_cast<long long>(tile) * NCOL;
+                redo_columns<512>(a, s, c0, c0 + NCOL, reinterpret_cast<uint16_t*>(qi_lds),
+                                  reinterpret_cast<uint32_t*>(qi_lds + kin * 2 * kRedoCols),
+                                  reinterpret_cast<uint32_t*>(qi_lds + kin * (2 * kRedoCols + 8)));
+            }
+        }
     };
 
     const bool rec = out_oor.counts != nullptr;
@@ -2219,6 +2277,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             if (done)
                 break;
         }
+        finish();
         return;
     }
     issue_rows(t0);
@@ -2264,6 +2323,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             nl[b ^ 1] = stage_marks(tile + 1, b ^ 1);
         __syncthreads();
     }
+    finish();
 }
 
 
@@ -2490,6 +2550,7 @@ static int gen_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 // operand-stationary kernel (KS = 8, 16): G row-block groups of 8 waves, C
 // column ranges per stripe; about two blocks per CU over the launch
 static constexpr bool kMmOs = true;
+constexpr long long kOsMaxTiles = 4096;  // tiles per block (slow-tile bitmask)
 
 template <int KS, int WR, int RPW>
 static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
@@ -2509,34 +2570,38 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
     // the XCD map wants S * C a multiple of 8
     while ((S * C) % 8 != 0 && C < TS / 2)
         C++;
+    // at most kOsMaxTiles tiles per block (the LDS bitmask of its slow
+    // tiles)
+    C = std::max(C, (TS + kOsMaxTiles - 1) / kOsMaxTiles);
     const long long blocks = static_cast<long long>(S) * G * C;
     if (blocks > 0x7fffffffLL)
         return -1;
+    constexpr size_t lds = O::kLds + kOsMaxTiles / 8;
     static std::atomic<uint64_t> attr_done{0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess)
         return -2;
     const uint64_t bit = dev < 64 ? 1ull << dev : 0;
-    if (O::kLds > 65536 && (!bit || !(attr_done.load(std::memory_order_acquire) & bit))) {
+    if (lds > 65536 && (!bit || !(attr_done.load(std::memory_order_acquire) & bit))) {
         if (hipFuncSetAttribute(
                 reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, true>),
-                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(O::kLds)) !=
+                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) !=
                 hipSuccess ||
             hipFuncSetAttribute(
                 reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, false>),
                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                static_cast<int>(O::kLds)) != hipSuccess)
+                static_cast<int>(lds)) != hipSuccess)
             return -2;
         attr_done.fetch_or(bit, std::memory_order_release);
     }
     a.tiles = static_cast<int>(TS);
     if (a.src.base1)
         hipLaunchKernelGGL((matrix_os_kernel<KS, WR, RPW, true>),
-                           dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), O::kLds, st,
+                           dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), lds, st,
                            a, G, static_cast<int>(C), static_cast<int>(TS));
     else
         hipLaunchKernelGGL((matrix_os_kernel<KS, WR, RPW, false>),
-                           dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), O::kLds, st,
+                           dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), lds, st,
                            a, G, static_cast<int>(C), static_cast<int>(TS));
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -2628,8 +2693,9 @@ bool matrix_cores_take(const RowSrc& src, const RowDst& dst, int R, long long wo
            words >= kRouteTile;
 }
 
-static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
+static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st, bool* dot2)
 {
+    *dot2 = false;
     const MatLayout& L = a.L;
     const RowSrc& src = a.src;
     const RowDst& dst = a.dst;
@@ -2661,6 +2727,7 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st)
             return rc;
         a.ext.c0 = wfull;
     }
+    *dot2 = true;
     switch (L.KP) {
     case 2:
         return mat_dispatch<2>(cols, a, S, st);
@@ -2715,9 +2782,10 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
         const int cols = L.KP <= 8 ? 4 : L.KP <= 16 ? 2 : 1;
         r += std::string(r.empty() ? "" : " + ") + "matrix_kernel<" + std::to_string(L.KP) +
              ", " + std::to_string(cols) + ", true> (tail)";
+        // the dot2 kernel's slow tiles (the matrix cores redo their own)
+        if (in_oor)
+            r += " + matrix_redo_kernel";
     }
-    if (in_oor)
-        r += " + matrix_redo_kernel";
     return r;
 }
 
@@ -2743,10 +2811,12 @@ int launch_matrix(const MatLayout& L, const int32_t* mat, long long ms,
     const Oor none{nullptr, nullptr, 0, 0};
     MatArgs a{L, mat, ms, ids, is, src, dst, mat_ext(src, L.R, dst, words), words, 0, in_oor ? *in_oor : none, slot_base, out_oor ? *out_oor : none,
               rowmap, route, rstride, in_oor ? slow : SlowList{nullptr, 0}, err};
-    const int rc = launch_matrix_kernels(a, S, st);
-    if (rc || !in_oor)
+    bool dot2 = false;
+    const int rc = launch_matrix_kernels(a, S, st, &dot2);
+    if (rc || !in_oor || !dot2)
         return rc;
-    // tiles with more marks than the kernels' LDS list: see push_slow_tile
+    // the dot2 kernel's tiles with more marks than its LDS list (the matrix
+    // cores redo theirs themselves): see push_slow_tile
     const int grid = (S + kRedoSpan - 1) / kRedoSpan;
     hipLaunchKernelGGL(matrix_redo_kernel, dim3(grid), dim3(kBlock), 0, st, a, S);
     return hipGetLastError() == hipSuccess ? 0 : -2;
