@@ -832,7 +832,41 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         if (mode == 0)
             Mt[(k - 1) * kp + tid] = 1;
         if (k <= 64) {
-            for (int j = k - 1; j >= 1; j--) {
+            // four coefficients per dependent step: from q = q_j,
+            //   q_{j-m} = c_m + x^m q_j,  c_1 = A[j], c_m = A[j-m+1] + x c_{m-1}
+            // (the c_m off the chain), and Horner's h the same way:
+            //   h' = q_{j-4} + x q_{j-3} + x^2 q_{j-2} + x^3 q_{j-1} + x^4 h
+            // (33 <= k <= 64; at k <= 32 the short chains measured faster
+            // one coefficient per step)
+            int j = k - 1;
+            if constexpr (NT == 256) {
+                const int32_t x2 = balanced(canon_lz(mul_lz(x, x)));
+                const int32_t x3 = balanced(canon_lz(mul_lz(x2, x)));
+                const int32_t x4 = balanced(canon_lz(mul_lz(x2, x2)));
+                for (; j >= 4; j -= 4) {
+                    const int32_t A1 = __builtin_amdgcn_readlane(ab0, j);
+                    const int32_t A2 = __builtin_amdgcn_readlane(ab0, j - 1);
+                    const int32_t A3 = __builtin_amdgcn_readlane(ab0, j - 2);
+                    const int32_t A4 = __builtin_amdgcn_readlane(ab0, j - 3);
+                    const int32_t c2 = A2 + mul_lz(x, A1);
+                    const int32_t c3 = A3 + mul_lz(x, c2);
+                    const int32_t c4 = A4 + mul_lz(x, c3);
+                    const int32_t q1 = fold(A1 + mul_lz(x, q));
+                    const int32_t q2 = fold(c2 + mul_lz(x2, q));
+                    const int32_t q3 = fold(c3 + mul_lz(x3, q));
+                    const int32_t q4 = fold(c4 + mul_lz(x4, q));
+                    if (mode == 0) {
+                        Mt[(j - 1) * kp + tid] = static_cast<uint32_t>(q1);
+                        Mt[(j - 2) * kp + tid] = static_cast<uint32_t>(q2);
+                        Mt[(j - 3) * kp + tid] = static_cast<uint32_t>(q3);
+                        Mt[(j - 4) * kp + tid] = static_cast<uint32_t>(q4);
+                    }
+                    const int32_t hs = q4 + mul_lz(x, q3) + mul_lz(x2, q2) + mul_lz(x3, q1);
+                    h = fold(hs + mul_lz(x4, h));
+                    q = q4;
+                }
+            }
+            for (; j >= 1; j--) {
                 q = __builtin_amdgcn_readlane(ab0, j) + mul_lz(q, x);
                 if (mode == 0)
                     Mt[(j - 1) * kp + tid] = static_cast<uint32_t>(q);

@@ -1143,7 +1143,6 @@ __global__ __launch_bounds__(64 * NW) void matrix_mfma_kernel(MatArgs a)
     const Oor out_oor = a.out_oor;
     const uint32_t* __restrict__ route = a.route;
     const long long route_stride = a.rstride;
-    const SlowList slow = a.slow;
     uint32_t* err = a.err;
     using G = MfmaTile<KS, NST, NW>;
     constexpr int NCOL = G::kCols, KH = G::kRows, RSB = G::kPitch;
