@@ -747,11 +747,20 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
 
     for (int i = k + tid; i < 2 * L.KP; i += NT)
         cids[i] = 0;
-    for (long long t = tid; t < ntiles; t += NT)
-        route[t * kRouteStride] = 0;
-    if (tid == 0) {
-        route[ntiles * kRouteStride] = 0;  // the slow-tile list starts empty
-        route[lazy_word_off(words)] = 0;   // no lazily filled section yet
+    // the route table belongs to the routing waves (1 .. NT / 64 - 1, while
+    // wave 0 builds A(x), below): tile t to wave 1 + t % nrw, which clears
+    // its count and then adds its marks -- a count cleared by another wave
+    // could land after marks were added (no barrier ahead of the chain)
+    constexpr int nrw = NT / 64 - 1;
+    const int rw = (tid >> 6) - 1, rl = tid & 63;
+    if (tid >= 64) {
+        for (long long t = rw + static_cast<long long>(nrw) * rl; t < ntiles; t += 64 * nrw)
+            route[t * kRouteStride] = 0;
+        if (tid == 64) {
+            route[ntiles * kRouteStride] = 0;  // the slow-tile list starts empty
+            route[lazy_word_off(words)] = 0;   // no lazily filled section yet
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's clears before its atomics
     }
     // x_i = r^{id_i}: thread tid takes point tid (its Q chain below); wave 0
     // also point 64 + lane (its A(x) chain reads every point by readlane)
@@ -797,8 +806,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
             A[k] = 1;
     } else if (in_oor.counts) {
         // route the received rows' OOR marks into per-tile tables (the
-        // other waves, while wave 0 builds A(x))
-        for (int i = tid - 64; i < k; i += NT - 64) {
+        // other waves, while wave 0 builds A(x)): every row's marks, each
+        // wave adding those of its own tiles
+        for (int i = rl; i < k; i += 64) {
             const int id = ids[static_cast<long long>(s) * k + i];
             const int slot = (by_pos ? i : id) - slot_base;
             if (slot < 0)
@@ -811,7 +821,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
             }
             for (uint32_t e = 0; e < c; e++) {
                 const uint32_t w = in_oor.entries[bk * in_oor.cap + e];
-                if (w >= words)
+                if (w >= words || static_cast<int>((w / kRouteTile) % nrw) != rw)
                     continue;
                 uint32_t* rt = route + (w / kRouteTile) * kRouteStride;
                 const uint32_t p = atomicAdd(rt, 1u);

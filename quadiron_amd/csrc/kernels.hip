@@ -2560,39 +2560,74 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
         return -1;
     const int RB = a.L.RB();
     const int G = (RB + WR * RPW - 1) / (WR * RPW);
+    constexpr size_t lds = O::kLds + kOsMaxTiles / 8;
+    // per device, once: the dynamic-LDS attribute and the number of blocks
+    // the device holds at once (CUs x blocks per CU)
+    static std::atomic<uint64_t> attr_done{0};
+    static std::atomic<int> slots_of[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return -2;
+    const uint64_t bit = dev < 64 ? 1ull << dev : 0;
+    if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
+        if (lds > 65536 &&
+            (hipFuncSetAttribute(
+                 reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, true>),
+                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) !=
+                 hipSuccess ||
+             hipFuncSetAttribute(
+                 reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, false>),
+                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                 static_cast<int>(lds)) != hipSuccess))
+            return -2;
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, false>),
+                O::kThreads, lds) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                hipSuccess)
+            return -2;
+        if (bit) {
+            slots_of[dev].store(std::max(1, per_cu) * std::max(1, cus),
+                                std::memory_order_relaxed);
+            attr_done.fetch_or(bit, std::memory_order_release);
+        }
+    }
+    const long long slots = bit ? slots_of[dev].load(std::memory_order_relaxed) : 256;
     // blocks wanted over the launch: ~2 per CU, or ~8 for the short KS = 4
     // decodes (cfg3: two column ranges per stripe, 0.168 -> 0.158 ms; the
     // KS >= 8 decodes and generators lose at 2048, gpurun_out ab_x4)
     constexpr long long kTarget = KS == 4 ? 2048 : 512;
-    long long C = (kTarget + static_cast<long long>(S) * G - 1) / (static_cast<long long>(S) * G);
-    C = std::max(1LL, std::min(C, std::max(1LL, TS / 4)));
-    // the XCD map wants S * C a multiple of 8
+    const long long SG = static_cast<long long>(S) * G;
+    const long long cmax = std::max(1LL, TS / 4);
+    long long C = (kTarget + SG - 1) / SG;
+    C = std::max(1LL, std::min(C, cmax));
+    // the blocks are equal: a launch of B blocks takes ceil(B / slots)
+    // rounds, so among C .. 2C - 1 take the column-range count whose last
+    // round is fullest (k300 / k384: 576 blocks on 256 one-block CUs ran
+    // three rounds, the last a quarter full; 768 fill them), then let the
+    // XCD map have S * C a multiple of 8
+    {
+        long long best = C;
+        double best_eff = 0.0;
+        for (long long c = C; c < 2 * C && c <= cmax; c++) {
+            const long long B = SG * c;
+            const double eff = static_cast<double>(B) / (((B + slots - 1) / slots) * slots);
+            if (eff > best_eff + 1e-9) {
+                best_eff = eff;
+                best = c;
+            }
+        }
+        C = best;
+    }
     while ((S * C) % 8 != 0 && C < TS / 2)
         C++;
     // at most kOsMaxTiles tiles per block (the LDS bitmask of its slow
     // tiles)
     C = std::max(C, (TS + kOsMaxTiles - 1) / kOsMaxTiles);
-    const long long blocks = static_cast<long long>(S) * G * C;
+    const long long blocks = SG * C;
     if (blocks > 0x7fffffffLL)
         return -1;
-    constexpr size_t lds = O::kLds + kOsMaxTiles / 8;
-    static std::atomic<uint64_t> attr_done{0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess)
-        return -2;
-    const uint64_t bit = dev < 64 ? 1ull << dev : 0;
-    if (lds > 65536 && (!bit || !(attr_done.load(std::memory_order_acquire) & bit))) {
-        if (hipFuncSetAttribute(
-                reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, true>),
-                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) !=
-                hipSuccess ||
-            hipFuncSetAttribute(
-                reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, false>),
-                hipFuncAttributeMaxDynamicSharedMemorySize,
-                static_cast<int>(lds)) != hipSuccess)
-            return -2;
-        attr_done.fetch_or(bit, std::memory_order_release);
-    }
     a.tiles = static_cast<int>(TS);
     if (a.src.base1)
         hipLaunchKernelGGL((matrix_os_kernel<KS, WR, RPW, true>),

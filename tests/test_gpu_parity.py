@@ -69,7 +69,11 @@ def test_blocks_vs_reference_golden(hip_lib, name):
         rc, dec = fec_decode(hip_lib, k, m, sys_, g["outputs"], g["oor"],
                              g["oor_count"], g["missing"][p], g["data"])
         assert rc == 1
-        assert (dec == g["decoded"][p]).all()
+        bad = np.argwhere(dec != g["decoded"][p])
+        assert len(bad) == 0, (
+            f"pattern {p} (missing {np.flatnonzero(g['missing'][p]).tolist()}): "
+            f"{len(bad)} bytes differ, rows {np.unique(bad[:, 0]).tolist()}, "
+            f"bytes {bad[:8, 1].tolist()} .. {bad[-4:, 1].tolist()}")
 
 
 @pytest.mark.parametrize("name", golden_names("cabi_"))
