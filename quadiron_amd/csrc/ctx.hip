@@ -95,6 +95,52 @@ __device__ __forceinline__ uint32_t inv_lz(uint32_t xc)
     return canon_lz(mul_lz(t, e8));                    // x^65535
 }
 
+// balanced 1 / s for the small row scales s of the rare rescale (the search
+// tries s = 2, 3, ...; a powm per candidate had cost ~1 us of serial
+// multiplies each, with the whole block waiting at the next barrier)
+struct InvSmall {
+    int32_t v[64];
+};
+constexpr InvSmall make_inv_small()
+{
+    InvSmall t{};
+    for (uint32_t v = 1; v < 64; v++)
+        t.v[v] = balanced(powmod_c(v, 65535u));
+    return t;
+}
+__constant__ InvSmall kInvSmall = make_inv_small();
+__device__ __forceinline__ int32_t inv_small(uint32_t sc)
+{
+    return sc < 64 ? kInvSmall.v[sc] : balanced(powm(sc, 65535u));
+}
+
+// Synthetic-division steps q <- c[t + 1] + x q for t = t_hi down to t_lo,
+// f(t, q) after each (lazy: |c| <= 32768, |q| < 98400): eight coefficients
+// loaded ahead per group, so the LDS latency is paid once per eight steps
+// instead of on every step of the serial chain
+template <class F>
+__device__ __forceinline__ int32_t div_steps(const int32_t* c, int32_t x, int32_t q, int t_hi,
+                                             int t_lo, F&& f)
+{
+    int t = t_hi;
+    for (; t - 7 >= t_lo; t -= 8) {
+        int32_t a[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            a[u] = c[t + 1 - u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            q = a[u] + mul_lz(q, x);
+            f(t - u, q);
+        }
+    }
+    for (; t >= t_lo; t--) {
+        q = c[t + 1] + mul_lz(q, x);
+        f(t, q);
+    }
+    return q;
+}
+
 // NT threads: the Lagrange part runs on the first wave (lane = point); the
 // row packing and the MFMA operand tiles use every thread (NT = 256 for
 // k > 32, where they dominate and there are few stripes per launch).
@@ -145,7 +191,7 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
     uint32_t s = 1;
     while (bad) {  // rare; s, si and bad are uniform in the group
         s++;
-        const int32_t si = balanced(powm(s, 65535u));
+        const int32_t si = inv_small(s);
         if (iabs32(si) > 32766)
             continue;
         bad = 0;
@@ -189,7 +235,7 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
         f = f < 0 ? f + 65537 : f;
         const uint32_t sq = static_cast<uint32_t>(f >= 65537 ? f - 65537 : f);
         block[L.kcorr() + t] = static_cast<int32_t>(mulm(sq, 32768u));
-        block[L.rscale() + t] = s == 1 ? 1 : balanced(powm(s, 65535u));
+        block[L.rscale() + t] = s == 1 ? 1 : inv_small(s);
         if (L.KS()) {
             block[L.kmf() + t] = static_cast<int32_t>(mulm(sq, 32896u));
             block[L.rscale_mf() + t] = block[L.rscale() + t];
@@ -248,7 +294,7 @@ __device__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, c
             uint32_t sc = 1;
             while (bad) {  // rare; uniform in the group
                 sc++;
-                const int32_t si = balanced(powm(sc, 65535u));
+                const int32_t si = inv_small(sc);
                 if (iabs32(si) > 32766)
                     continue;
                 bad = 0;
@@ -289,7 +335,7 @@ __device__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, c
                 f = f < 0 ? f + 65537 : f;
                 const uint32_t sq = static_cast<uint32_t>(f >= 65537 ? f - 65537 : f);
                 mat[L.kcorr() + t] = static_cast<int32_t>(mulm(sq, 32768u));
-                const int32_t rs = sc == 1 ? 1 : balanced(powm(sc, 65535u));
+                const int32_t rs = sc == 1 ? 1 : inv_small(sc);
                 mat[L.rscale() + t] = rs;
                 mat[L.kmf() + t] = static_cast<int32_t>(mulm(sq, 32896u));
                 mat[L.rscale_mf() + t] = rs;
@@ -348,7 +394,7 @@ template <int NT, bool BIG>
 __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
     int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
-    int by_pos, long long words, int dot2, uint32_t* err)
+    int by_pos, long long words, int dot2, uint32_t* err, int nb)
 {
     __shared__ uint32_t xs[kMatMaxKin];
     __shared__ uint32_t A[kMatMaxKin + 1];
@@ -361,7 +407,12 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // reads 16 rows x 16 bytes per wave (ds_read_b128) conflict-free (the
     // odd pitch k | 1 had SQ_LDS_BANK_CONFLICT at 7.4 cycles per LDS
     // instruction at k = 64)
-    const int s = blockIdx.x;
+    // nb blocks per stripe (the non-systematic whole-tile form only; nb = 1
+    // otherwise): block cb builds the row chunks [c0, c1) of its stripe's
+    // matrix, block 0 also the ids and the route table; each computes A(x)
+    // and the A'(x_i) itself (few stripes per launch left most CUs idle
+    // behind one block per stripe: k300, 32 stripes, 147 us)
+    const int s = blockIdx.x / nb, cb = blockIdx.x - s * nb;
     const int tid = threadIdx.x;
     int32_t* mat = ctx + s * ctx_stride;
     // BIG (128 < k <= 256): the k x k matrix (up to 256 KB) does not fit
@@ -371,25 +422,28 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     uint32_t* Mt = BIG ? reinterpret_cast<uint32_t*>(mat + L.plain()) : qi_ctx_lds;
     int32_t* cids = mat + L.words();
     uint32_t* route = reinterpret_cast<uint32_t*>(cids + 2 * L.KP);
-    for (int i = k + tid; i < 2 * L.KP; i += NT)
-        cids[i] = 0;
+    const bool lead = cb == 0;  // block-uniform
     const long long ntiles = route_tiles(words);
-
-    // route table: clear, then (after the barrier below) fill; the
-    // slow-tile list behind it starts empty
-    for (long long t = tid; t < ntiles; t += NT)
-        route[t * kRouteStride] = 0;
-    if (tid == 0) {
-        route[ntiles * kRouteStride] = 0;
-        route[lazy_word_off(words)] = 0;  // no lazily filled section yet
+    if (lead) {
+        for (int i = k + tid; i < 2 * L.KP; i += NT)
+            cids[i] = 0;
+        // route table: clear, then (after the barrier below) fill; the
+        // slow-tile list behind it starts empty
+        for (long long t = tid; t < ntiles; t += NT)
+            route[t * kRouteStride] = 0;
+        if (tid == 0) {
+            route[ntiles * kRouteStride] = 0;
+            route[lazy_word_off(words)] = 0;  // no lazily filled section yet
+        }
     }
     if (tid < k) {
         const uint32_t id = ids[static_cast<long long>(s) * k + tid];
         xs[tid] = powm(r, id);
-        cids[tid] = static_cast<int32_t>(id);
+        if (lead)
+            cids[tid] = static_cast<int32_t>(id);
     }
     __syncthreads();
-    if (in_oor.counts && tid < k) {
+    if (lead && in_oor.counts && tid < k) {
         const int id = ids[static_cast<long long>(s) * k + tid];
         const int slot = (by_pos ? tid : id) - slot_base;
         if (slot >= 0) {
@@ -417,42 +471,92 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // ds_bpermute shifts and canonical mulm of round 2 took ~620 cycles per
     // step: 62 us of a k = 200 context).  A is monic: A[k] = 1 is set
     // explicitly, so k = 64 u needs no extra slot.  Stored balanced.
+    // (BIG: the product tree's levels, then the split Horner chains of the
+    // A'(x_i))
+    __shared__ int32_t pt[2][2 * 512 + 4];
     if constexpr (BIG) {
         // k > 128: A(x) by a product tree instead of k dependent steps on one
         // wave (k = 256: 256 steps x 4 coefficient slots of DPP shifts and
-        // products).  Level l holds NL >> l polynomials of degree <= 2^l
-        // (2^l + 1 balanced coefficients each); leaf i is x - x_i, or 1 past
-        // k.  One thread per output coefficient of a level: its <= 2^l + 1
-        // lazy products (|sum| < 2^25), folded and stored balanced.  The
-        // critical path is ~NL products and log2 NL barriers.
-        __shared__ int32_t pt[2][2 * 512 + 4];
-        int NL = 1, lgl = 0;
-        while (NL < k) {
-            NL <<= 1;
-            lgl++;
+        // products).  Leaves: wave w multiplies out the points [w g, w g +
+        // g), g = ceil(k / 16) <= 24, as the k <= 64 kernel does (lane d
+        // holds coefficient d; the shift by DPP, x_i by readlane).  Then 4
+        // levels of pairwise products (16 -> 1 polynomials of span g 2^l
+        // points, slots of g 2^l + 1 balanced coefficients): each pair's
+        // outer product in 4 x 4 tiles, one per thread, its 7 anti-diagonal
+        // sums added into the level by LDS atomics (|sum| < 2^24), then
+        // folded and stored balanced; tiles past the children's true degrees
+        // are skipped.  (One thread per coefficient of a 2-leaf tree left the
+        // top levels serial: 257 + 129 + ... products, 31 of a k300
+        // context's 147 us; the 9-level tiled tree still took 14.)
+        constexpr int NWV = NT / 64;
+        static_assert(NWV == 16, "16 leaf polynomials");
+        const int g = (k + NWV - 1) / NWV;  // <= 24 (k <= 384)
+        {
+            const int w = tid >> 6, ln = tid & 63;
+            const int p0 = w * g, cnt = max(0, min(k, p0 + g) - p0);
+            const int32_t xv = ln < cnt ? balanced(xs[p0 + ln]) : 0;
+            int32_t a = ln == 0 ? 1 : 0;
+            for (int i = 0; i < cnt; i++) {
+                const int32_t x = __builtin_amdgcn_readlane(xv, i);
+                const int32_t prev = __builtin_amdgcn_update_dpp(0, a, 0x138, 0xf, 0xf, false);
+                a = fold(prev - mul_lz(a, x));
+            }
+            if (ln <= g)
+                pt[0][w * (g + 1) + ln] = balanced(canon_lz(a));
         }
-        for (int i = tid; i < NL; i += NT) {
-            pt[0][2 * i] = i < k ? -balanced(xs[i]) : 1;
-            pt[0][2 * i + 1] = i < k ? 1 : 0;
-        }
-        __syncthreads();
-        int cur = 0;
-        for (int lv = 0; lv < lgl; lv++) {
-            const int D = (1 << lv) + 1, D2 = (2 << lv) + 1, np = NL >> (lv + 1);
+        int cur = 0, D = g + 1, span = g;
+        for (int m = NWV; m > 1; m >>= 1) {
+            const int np = m / 2, D2 = 2 * D - 1;
             const int32_t* in = pt[cur];
             int32_t* out = pt[cur ^ 1];
-            for (int it = tid; it < np * D2; it += NT) {
-                const int pp = it / D2, m = it - pp * D2;
+            for (int it = tid; it < np * D2; it += NT)
+                out[it] = 0;
+            __syncthreads();
+            // the live tiles only: rows u <= degL / 4, columns v <= degR / 4
+            // of each pair (np <= 8 pairs, scanned per tile)
+            auto deg = [&](int c) { return min(max(k - c * span, 0), span); };
+            int total = 0;
+            for (int pp = 0; pp < np; pp++)
+                total += (deg(2 * pp) / 4 + 1) * (deg(2 * pp + 1) / 4 + 1);
+            for (int it = tid; it < total; it += NT) {
+                int pp = 0, r0 = it, tv = deg(1) / 4 + 1;
+                for (int c = (deg(0) / 4 + 1) * tv; r0 >= c; c = (deg(2 * pp) / 4 + 1) * tv) {
+                    r0 -= c;
+                    pp++;
+                    tv = deg(2 * pp + 1) / 4 + 1;
+                }
+                const int u = r0 / tv, v = r0 - u * tv;
+                const int degL = deg(2 * pp), degR = deg(2 * pp + 1);
                 const int32_t* Lp = in + (2 * pp) * D;
                 const int32_t* Rp = Lp + D;
-                const int a0 = m - (D - 1) > 0 ? m - (D - 1) : 0, a1 = m < D - 1 ? m : D - 1;
-                int32_t acc = 0;
-                for (int a = a0; a <= a1; a++)
-                    acc += mul_lz(Lp[a], Rp[m - a]);
-                out[pp * D2 + m] = balanced(canon_lz(fold(acc)));
+                int32_t la[4], rb[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    la[j] = 4 * u + j <= degL ? Lp[4 * u + j] : 0;
+                    rb[j] = 4 * v + j <= degR ? Rp[4 * v + j] : 0;
+                }
+                int32_t acc[7];
+#pragma unroll
+                for (int d = 0; d < 7; d++)
+                    acc[d] = 0;
+#pragma unroll
+                for (int a = 0; a < 4; a++)
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        acc[a + b] += mul_lz(la[a], rb[b]);
+                int32_t* o = out + pp * D2 + 4 * (u + v);
+#pragma unroll
+                for (int d = 0; d < 7; d++)
+                    if (4 * (u + v) + d < D2)
+                        atomicAdd(o + d, acc[d]);
             }
             __syncthreads();
+            for (int it = tid; it < np * D2; it += NT)
+                out[it] = balanced(canon_lz(fold(out[it])));
+            __syncthreads();
             cur ^= 1;
+            D = D2;
+            span *= 2;
         }
         for (int i = tid; i < k; i += NT)
             A[i] = static_cast<uint32_t>(pt[cur][i]);
@@ -504,7 +608,44 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             A[k] = 1;
     }
     __syncthreads();
-    if (tid < k) {
+    // (the chunked BIG rows are written by a second division below)
+    const bool rows = mode == 0 && !(BIG && !dot2);
+    if (BIG && !rows) {
+        // only the A'(x_i): the derivative's coefficients d_j = (j + 1)
+        // A[j + 1], then PP = NT / k threads per point, each a Horner chain
+        // over a k / PP slice of them, combined with powers x^len (the one
+        // k-step chain per point took 17 of a k300 context's 147 us)
+        int32_t* dA = pt[0];
+        int32_t* part = pt[1];
+        const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
+        for (int j = tid; j < k; j += NT)
+            dA[j] = balanced(canon_lz(mul_lz(j + 1, Ab[j + 1])));
+        __syncthreads();
+        const int PP = NT / k, len = (k + PP - 1) / PP;
+        if (tid < PP * k) {
+            const int pq = tid / k, i = tid - pq * k;
+            const int32_t x = balanced(xs[i]);
+            const int lo = pq * len, hi = min(k, lo + len);
+            // h <- dA[j] + x h for j = hi - 1 .. lo (|h| < 98400)
+            part[pq * k + i] = div_steps(dA - 1, x, 0, hi - 1, lo, [](int, int32_t) {});
+        }
+        __syncthreads();
+        if (tid < k) {
+            const int32_t x = balanced(xs[tid]);
+            int32_t xl = 1, b = x;
+            for (int e = len; e; e >>= 1) {
+                if (e & 1)
+                    xl = mul_lz(xl, b);
+                b = mul_lz(b, b);
+            }
+            int32_t h = part[(PP - 1) * k + tid];
+            for (int pq = PP - 2; pq >= 0; pq--)
+                h = fold(part[pq * k + tid] + mul_lz(h, xl));
+            const uint32_t ap = canon_lz(fold(h));
+            aprime[tid] = ap;
+            cinv[tid] = inv_lz(ap);
+        }
+    } else if (tid < k) {
         // Q_i = A / (x - x_i) by synthetic division from the top, and
         // A'(x_i) = Q_i(x_i) by Horner beside it (two interleaved chains),
         // lazy as in decode_ctx_lds_kernel (|q| < 98400, |h| < 2^18); the
@@ -513,8 +654,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         const int32_t xi = balanced(xs[tid]);
         const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
         int32_t q = 1, h = 1;  // A[k]; Q_i(x_i) so far
-        // (the chunked BIG rows are written by a second division below)
-        const bool rows = mode == 0 && !(BIG && !dot2);
         if (rows)
             Mt[(k - 1) * kp + tid] = 1;
         for (int j = k - 1; j >= 1; j--) {
@@ -576,15 +715,20 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             const int kpc = (k + 3) & ~3;
             const int32_t xi = tid < k ? balanced(xs[tid]) : 0;
             const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
-            int32_t q = 1;
-            for (int c = (k - 1) / kCtxChunk; c >= 0; c--) {
+            // this block's chunks [c0, c1): the division runs down from the
+            // top through the rows above them without keeping them
+            const int nch = (k + kCtxChunk - 1) / kCtxChunk;
+            const int c0 = (cb * nch + nb - 1) / nb, c1 = ((cb + 1) * nch + nb - 1) / nb;
+            int32_t q = 1;  // coef_{k-1}(Q_i)
+            if (tid < k)
+                q = div_steps(Ab, xi, q, k - 2, kCtxChunk * c1, [](int, int32_t) {});
+            for (int c = c1 - 1; c >= c0; c--) {
                 const int lo = kCtxChunk * c, hi = min(k, lo + kCtxChunk);
                 if (tid < k) {
-                    for (int t = hi - 1; t >= lo; t--) {
-                        if (t < k - 1)
-                            q = Ab[t + 1] + mul_lz(q, xi);
-                        ch[(t - lo) * kpc + tid] = canon_lz(q);
-                    }
+                    auto keep = [&](int t, int32_t qt) { ch[(t - lo) * kpc + tid] = canon_lz(qt); };
+                    if (hi == k)
+                        keep(k - 1, q);
+                    q = div_steps(Ab, xi, q, hi == k ? k - 2 : hi - 1, lo, keep);
                 }
                 __syncthreads();
                 auto ent = [&](int t, int i0, uint32_t (&e)[4]) {
@@ -966,8 +1110,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
                 uint32_t sc = 0;
                 for (uint32_t cand = 2; cand < 256 && !sc; cand++) {
                     // |s^-1| <= 32766 (the epilogue's v_mul_i32_i24)
-                    const uint32_t ci = inv_lz(cand);
-                    if (ci - 32767u < 4u)
+                    const int32_t ci = inv_small(cand);
+                    if (iabs32(ci) > 32766)
                         continue;
                     uint32_t fail = 0;
                     for (int i = sub; i < k; i += 4)
@@ -976,7 +1120,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
                     fail |= __builtin_amdgcn_update_dpp(0u, fail, 0x4E, 0xf, 0xf, false);
                     if (!fail) {
                         sc = cand;
-                        rs = balanced(ci);
+                        rs = ci;
                     }
                 }
                 if (!sc)  // never seen (p ~ 2^-1000): mark the stripe undecodable
@@ -1141,11 +1285,18 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
                                ? static_cast<size_t>(kCtxChunk) * ((k + 3) & ~3) * 4
                                : 0;
         static std::atomic<uint64_t> attr_done{0};
+        static std::atomic<int> cus_of[64];
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess)
             return -2;
         const uint64_t bit = dev < 64 ? 1ull << dev : 0;
         if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                hipSuccess)
+                return -2;
+            if (bit)
+                cus_of[dev].store(std::max(1, cus), std::memory_order_relaxed);
             const void* fn = reinterpret_cast<const void*>(&decode_ctx_kernel<1024, true>);
             constexpr size_t kDynMax = static_cast<size_t>(kCtxChunk) * kMatMaxKin * 4;
             // the kernel's static LDS (the packing stage, A, x_i, ...) plus
@@ -1160,9 +1311,19 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
                 return -2;
             attr_done.fetch_or(bit, std::memory_order_release);
         }
-        hipLaunchKernelGGL((decode_ctx_kernel<1024, true>), dim3(S), dim3(1024), lds, st, k, r,
-                           mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
-                           slot_base, by_pos, words, dot2, err);
+        // the non-systematic whole-tile form splits a stripe's row chunks
+        // over up to (CUs / stripes) blocks (one block per CU each)
+        int nb = 1;
+        if (mode == 0 && !dot2) {
+            const int cus = bit ? cus_of[dev].load(std::memory_order_relaxed) : 256;
+            const int nch = (k + kCtxChunk - 1) / kCtxChunk;
+            nb = std::max(1, std::min(nch, cus / S));
+        }
+        if (static_cast<long long>(S) * nb > 0x7fffffffLL)
+            return -1;
+        hipLaunchKernelGGL((decode_ctx_kernel<1024, true>), dim3(S * nb), dim3(1024), lds, st, k,
+                           r, mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
+                           slot_base, by_pos, words, dot2, err, nb);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     RPow2 rp{};
