@@ -262,6 +262,10 @@ def parse_args(argv=None):
     ap.add_argument("--systematic", action="store_true")
     ap.add_argument("--chunks", type=int, default=1)
     ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--ctx-stream", type=int, default=None, choices=(0, 1),
+                    help="build the decode contexts from the ids alone on a "
+                         "second stream beside the encode (default: off, "
+                         "see CTX_STREAM)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the cfg3 line the default (cfg2) run appends")
@@ -313,7 +317,8 @@ def main(argv=None):
 
     res = run_config(args.cfg, args.stripes, bool(args.systematic), args.steps,
                      args.warmup, NC=max(1, args.chunks), n_streams=args.streams,
-                     dist=dist, dev=dev, dry=dry, rank=rank, world=world)
+                     dist=dist, dev=dev, dry=dry, rank=rank, world=world,
+                     ctx_stream=args.ctx_stream)
     out = report(res, args.cfg, world, args.steps, args.warmup, dry)
     ok = res["ok"]
     # BASELINE.json configs[2] (k=64 n=1024 pkt=4KiB, 1024 stripes) in the
@@ -349,8 +354,18 @@ def main(argv=None):
         sys.exit(3)
 
 
+# configurations whose step builds the decode contexts on a second stream,
+# from the ids alone, while the encode runs (init_context_dec before the
+# fragments exist; the decode then reads the OOR marks from the buckets).
+# None by default: measured slower everywhere (cfg3 4.45-4.58 vs 4.79-4.84
+# TB/s: the encode 0.95-0.98 vs 0.91 ms beside the context blocks, the
+# bucket-scanning decode 0.141-0.146 vs 0.134 ms; cfg2 6.04 vs 6.23;
+# gpurun_out/ab_r5i_*, profiles/r5_ab_notes.txt)
+CTX_STREAM = set()
+
+
 def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
-               dev=None, dry=False, rank=0, world=1):
+               dev=None, dry=False, rank=0, world=1, ctx_stream=None):
     """Build one configuration's synthetic batch in HBM, run `warmup`
     untimed steps, check the round trip, then time exactly `steps` steps
     between barriers + device synchronisations (max over ranks).  One step =
@@ -368,6 +383,8 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
     assert S % NC == 0, "stripes must divide into chunks"
     C = S // NC
     ev = []
+    overlap = (cfg in CTX_STREAM) if ctx_stream is None else bool(ctx_stream)
+    overlap = overlap and NC == 1 and not dry
 
     if dry:
         # the same loop structure on a small CPU stand-in per step
@@ -405,6 +422,7 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
         streams = ([torch.cuda.current_stream()] if NC == 1 else
                    [torch.cuda.Stream() for _ in range(max(1, n_streams))])
         cstride = plan.ctx_bytes(1, P)
+        cst = torch.cuda.Stream() if overlap else None
 
         def step(timed):
             for j in range(NC):
@@ -419,13 +437,30 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
                         # HIP events on the launch stream itself
                         e0, e1, ec, e2 = (torch.cuda.Event(enable_timing=True)
                                           for _ in range(4))
+                    if overlap:
+                        # the contexts from the ids alone on their own
+                        # stream, beside the encode (after the previous
+                        # step's decode, their last reader)
+                        cst.wait_stream(st)
+                        with torch.cuda.stream(cst):
+                            if timed:
+                                c0, c1 = (torch.cuda.Event(enable_timing=True)
+                                          for _ in range(2))
+                                c0.record(cst)
+                            plan.decode_ctx(ids[a:b], cx, P, stream=cst.cuda_stream)
+                            if timed:
+                                c1.record(cst)
+                    if timed:
                         e0.record(st)
                     plan.encode(data[a:b], coded[a:b], cnt, ent, cap,
                                 stream=st.cuda_stream)
                     if timed:
                         e1.record(st)
-                    plan.decode_ctx(ids[a:b], cx, P, cnt, ent, cap,
-                                    stream=st.cuda_stream)
+                    if overlap:
+                        st.wait_stream(cst)
+                    else:
+                        plan.decode_ctx(ids[a:b], cx, P, cnt, ent, cap,
+                                        stream=st.cuda_stream)
                     if timed:
                         ec.record(st)
                     plan.decode(cx, ids[a:b], coded[a:b], dec[a:b],
@@ -433,7 +468,7 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
                                 cap=cap, stream=st.cuda_stream, check=False)
                     if timed:
                         e2.record(st)
-                        ev.append((e0, e1, ec, e2))
+                        ev.append((e0, e1, ec, e2, (c0, c1) if overlap else None))
 
         def check():
             # every stripe decoded back to its data, no OOR bucket overflowed
@@ -475,16 +510,21 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
         elapsed, ok = reduce_over_ranks(dist, elapsed, ok, dev)
     enc_ms = dec_ms = ctx_ms = None  # dry run: no kernels
     if ev:
-        enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _, _ in ev]))
-        ctx_ms = float(np.mean([b.elapsed_time(c) for _, b, c, _ in ev]))
-        dec_ms = float(np.mean([b.elapsed_time(d) for _, b, _, d in ev]))
+        enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _, _, _ in ev]))
+        # overlapped: the context kernel's own time on its stream (not on
+        # the step's critical path); the decode time runs from the encode's
+        # end to the decode's end either way
+        ctx_ms = float(np.mean([c[0].elapsed_time(c[1]) if c else b.elapsed_time(cc)
+                                for _, b, cc, _, c in ev]))
+        dec_ms = float(np.mean([b.elapsed_time(d) for _, b, _, d, _ in ev]))
     # the kernels this plan launches (the library's own dispatch,
     # qi_gpu_kernels); the dry run names the cfg2 kernels it stands in for
     if dry:
         kernels = "encode=encode_fnt_kernel<16,2>; decode=(dry run: none)"
     else:
         kernels = plan.kernels(P)
-    return {"k": k, "m": m, "n": n, "P": P, "pkt_bytes": pkt_bytes, "S": S,
+    return {"ctx_overlap": overlap,
+            "k": k, "m": m, "n": n, "P": P, "pkt_bytes": pkt_bytes, "S": S,
             "C": C, "NC": NC, "sys": sys_, "steps": steps, "elapsed": elapsed,
             "ok": ok, "enc_ms": enc_ms, "dec_ms": dec_ms, "ctx_ms": ctx_ms,
             "kernels": kernels, "streams": len(streams)}
@@ -575,7 +615,10 @@ def report(res, cfg, world, steps, warmup, dry):
             "systematic": sys_,
             "stripes_per_gpu": S,
             "decode": "per-stripe random n-k erasures, contexts built "
-                      "on-GPU inside the timed step",
+                      "on-GPU inside the timed step" +
+                      (" (from the ids on a second stream, beside the encode; "
+                       "the decode reads the OOR marks from the buckets)"
+                       if res.get("ctx_overlap") else ""),
             "parallelism": f"stripe-sharded x{world} (no collective)",
             "chunks": res["NC"], "streams": res["streams"],
         },

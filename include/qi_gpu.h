@@ -92,8 +92,12 @@ size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
  * d_ids[s*k + i] (u16, ascending, distinct, < k+m) -- the k fragments the
  * decoder uses (FecCode::decode_blocks_vertical picks the first k present,
  * src/fec_base.h:1199-1236) -- and route the OOR marks of those fragments
- * (buckets as produced by qi_gpu_encode; NULL counts = none) into per-tile
- * tables.  Built on the device, asynchronously on `stream`, for every k:
+ * (buckets as produced by qi_gpu_encode) into per-tile tables.  With NULL
+ * counts the context is built from the ids alone (init_context_dec,
+ * src/fec_base.h:758-793: before the fragments' data and marks exist, e.g.
+ * on another stream while they are produced); a decode given buckets then
+ * reads the marks from them directly (slightly slower per tile than routed
+ * tables).  Built on the device, asynchronously on `stream`, for every k:
  * matrix contexts (the interpolation matrix, up to ~780 KB per stripe at
  * k = 256) for k <= 256, and for 256 < k <= 384 at widths that are a
  * multiple of 1024 columns (then followed by the NTT engine's context, used

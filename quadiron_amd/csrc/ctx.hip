@@ -428,9 +428,13 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         for (int i = k + tid; i < 2 * L.KP; i += NT)
             cids[i] = 0;
         // route table: clear, then (after the barrier below) fill; the
-        // slow-tile list behind it starts empty
+        // slow-tile list behind it starts empty.  A context built without
+        // the buckets (ids only: init_context_dec, src/fec_context.h) marks
+        // every tile unrouted (count > kRouteCap): a decode given marks then
+        // scans the buckets itself
+        const uint32_t rt0 = in_oor.counts ? 0u : static_cast<uint32_t>(kRouteCap) + 1u;
         for (long long t = tid; t < ntiles; t += NT)
-            route[t * kRouteStride] = 0;
+            route[t * kRouteStride] = rt0;
         if (tid == 0) {
             route[ntiles * kRouteStride] = 0;
             route[lazy_word_off(words)] = 0;  // no lazily filled section yet
@@ -898,8 +902,10 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
     constexpr int nrw = NT / 64 - 1;
     const int rw = (tid >> 6) - 1, rl = tid & 63;
     if (tid >= 64) {
+        // (ids only, no buckets: every tile unrouted, as decode_ctx_kernel)
+        const uint32_t rt0 = in_oor.counts ? 0u : static_cast<uint32_t>(kRouteCap) + 1u;
         for (long long t = rw + static_cast<long long>(nrw) * rl; t < ntiles; t += 64 * nrw)
-            route[t * kRouteStride] = 0;
+            route[t * kRouteStride] = rt0;
         if (tid == 64) {
             route[ntiles * kRouteStride] = 0;  // the slow-tile list starts empty
             route[lazy_word_off(words)] = 0;   // no lazily filled section yet

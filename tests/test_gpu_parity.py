@@ -249,6 +249,16 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True,
     assert err == 0
     dec_h = dec.cpu().numpy().view(np.uint16)
     assert (dec_h == data).all()
+    # a context from the ids alone (no buckets: init_context_dec before the
+    # marks exist); the decode reads the marks from the buckets itself
+    ctx3 = torch.randint(0, 256, (plan.ctx_bytes(S, P),), dtype=torch.uint8,
+                         device="cuda")
+    plan.decode_ctx(di, ctx3, P, h_ids=ids)
+    dec3 = torch.zeros_like(dec)
+    assert plan.decode(ctx3, di, out, dec3, data=dd, counts=counts,
+                       entries=entries, cap=cap) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dec3, dd)
     for s in oracle_stripes or ():
         ent_s = ent_h[s].copy()
         for i in range(no):  # the buckets are unordered; the oracle's ascend

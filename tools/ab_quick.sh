@@ -14,7 +14,7 @@ for i in 1 2 3; do
     L=quadiron_amd/libquadiron_amd.so; [ $v != main ] && L=build/ab/$v/libquadiron_amd.so
     for c in $CFGS; do
       F="--cfg ${c%:sys}"; [ "${c%:sys}" != "$c" ] && F="$F --systematic"
-      QI_LIB_PATH=$L timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-secondary --steps 20 ${AB_WARMUP:+--warmup $AB_WARMUP} $F > $O/${v}_${c}_$i.log 2>&1
+      QI_LIB_PATH=$L timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-secondary --steps 20 ${AB_WARMUP:+--warmup $AB_WARMUP} $F $AB_ARGS > $O/${v}_${c}_$i.log 2>&1
       rc=$?
       # a probe variant (results deliberately wrong) exits 3 after its line;
       # anything else (no bench line, a fault, a time limit) ends the run
