@@ -262,6 +262,9 @@ def parse_args(argv=None):
     ap.add_argument("--systematic", action="store_true")
     ap.add_argument("--chunks", type=int, default=1)
     ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--timed-events", action="store_true",
+                    help="record the per-kernel HIP events on the timed steps "
+                         "(default: on the last warmup steps)")
     ap.add_argument("--ctx-stream", type=int, default=None, choices=(0, 1),
                     help="build the decode contexts from the ids alone on a "
                          "second stream beside the encode (default: off, "
@@ -318,7 +321,7 @@ def main(argv=None):
     res = run_config(args.cfg, args.stripes, bool(args.systematic), args.steps,
                      args.warmup, NC=max(1, args.chunks), n_streams=args.streams,
                      dist=dist, dev=dev, dry=dry, rank=rank, world=world,
-                     ctx_stream=args.ctx_stream)
+                     ctx_stream=args.ctx_stream, timed_events=args.timed_events)
     out = report(res, args.cfg, world, args.steps, args.warmup, dry)
     ok = res["ok"]
     # BASELINE.json configs[2] (k=64 n=1024 pkt=4KiB, 1024 stripes) in the
@@ -365,7 +368,7 @@ CTX_STREAM = set()
 
 
 def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
-               dev=None, dry=False, rank=0, world=1, ctx_stream=None):
+               dev=None, dry=False, rank=0, world=1, ctx_stream=None, timed_events=False):
     """Build one configuration's synthetic batch in HBM, run `warmup`
     untimed steps, check the round trip, then time exactly `steps` steps
     between barriers + device synchronisations (max over ranks).  One step =
@@ -486,9 +489,15 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
     # idle for a few ms, and the timed steps then started at a lower clock
     # (cfg3 encode 1.03-1.05 ms over 20 steps vs 0.925 steady,
     # tools/ramp.py)
+    # the kernel times come from HIP events on the last n_ev warmup steps,
+    # which run back to back into the timed region: event markers between
+    # the kernels of a timed step added launch bubbles to the wall time
+    # (--timed-events: on the timed steps instead, as before)
+    # (not the first warmup step, which is followed by the host-side check)
+    n_ev = 0 if timed_events else min(10, warmup - 1 if warmup > 1 else warmup)
     ok = True
     for w in range(warmup):
-        step(False)
+        step(w >= warmup - n_ev)
         if w == 0:
             sync()
             ok = check()  # the measured pipeline, outside the timed region
@@ -499,7 +508,7 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step(True)
+        step(n_ev == 0)
     sync()
     if dist:
         dist.barrier()
@@ -523,7 +532,10 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
         kernels = "encode=encode_fnt_kernel<16,2>; decode=(dry run: none)"
     else:
         kernels = plan.kernels(P)
-    return {"ctx_overlap": overlap,
+    return {"ctx_overlap": overlap, "events_on": (
+                "timed steps" if n_ev == 0 else
+                f"warmup steps {warmup - n_ev}..{warmup - 1} (back to back into "
+                f"the timed region, which runs without event markers)"),
             "k": k, "m": m, "n": n, "P": P, "pkt_bytes": pkt_bytes, "S": S,
             "C": C, "NC": NC, "sys": sys_, "steps": steps, "elapsed": elapsed,
             "ok": ok, "enc_ms": enc_ms, "dec_ms": dec_ms, "ctx_ms": ctx_ms,
@@ -628,6 +640,7 @@ def report(res, cfg, world, steps, warmup, dry):
         "encode_GBps": enc_gbs,
         "decode_ms": dec_ms,
         "decode_ctx_ms": ctx_ms,
+        "kernel_times_from": res.get("events_on"),
         "decode_GBps": dec_gbs,
         "roundtrip_ok": res["ok"],
         # the dominant kernel: the encode (one launch per encode call at
