@@ -1937,7 +1937,11 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     int32_t kt[RPW], rs[RPW], pr[RPW][3];
 #pragma unroll
     for (int j = 0; j < RPW; j++) {
-        const int rb = gq * WR * RPW + slot + WR * j;
+        // row blocks dealt round-robin over the G groups (their counts
+        // differ by at most one): a group with fewer busy waves ran ahead of
+        // the others, and the input tiles it had fetched were evicted from
+        // L2 before they came by (k300: 1.88x the input bytes read)
+        const int rb = gq + G * (slot + WR * j);
         act[j] = rb < RB;  // wave-uniform
         const int rbc = act[j] ? rb : RB - 1;
         rbj[j] = rbc;
@@ -2645,10 +2649,19 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 struct OsGeom {
     int wr, rpw;
 };
-inline OsGeom os_geom(int KS, int RB)
+inline OsGeom os_geom(int KS, int RB, bool two)
 {
     if (!kMmOs)
         return {0, 0};
+    // KS = 16, 20 with more than one block of 8 row blocks, one source
+    // region: two row blocks per wave, so one group (k200, k256) or two
+    // (k300) stage each input tile instead of two or three (k200 decode
+    // 0.757 -> 0.66 ms, k300 0.704 -> 0.653, k256 0.30 -> 0.278; encodes
+    // 10 % faster).  Not at KS = 24 (256 VGPRs and scratch), nor for the
+    // systematic decodes' two regions (k300 sys decode 1.05 -> 1.41 ms), nor
+    // at KS = 8 (k128 encode 0.725 -> 0.757 ms; gpurun_out/ab_r5k)
+    if ((KS == 16 || KS == 20) && RB > 8 && !two)
+        return {8, 2};
     if (KS >= 8)
         return {8, 1};
     // KS = 4: the short decode matrices (2 super tiles per 128-column tile)
@@ -2664,13 +2677,22 @@ template <int KS>
 static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t st)
 {
     if constexpr (KS == 4) {
-        const OsGeom og = os_geom(KS, a.L.RB());
+        const OsGeom og = os_geom(KS, a.L.RB(), a.src.base1 != nullptr);
         if (og.wr == 4 && og.rpw == 1)
             return os_launch<KS, 4, 1>(a, wfull, S, st);
         if (og.wr == 8 && og.rpw == 1)
             return os_launch<KS, 8, 1>(a, wfull, S, st);
-    } else if constexpr (KS == 8 || KS == 16 || KS == 20 || KS == 24) {
-        if (os_geom(KS, a.L.RB()).wr)
+    } else if constexpr (KS == 8) {
+        if (os_geom(KS, a.L.RB(), a.src.base1 != nullptr).wr)
+            return os_launch<KS, 8, 1>(a, wfull, S, st);
+    } else if constexpr (KS == 16 || KS == 20) {
+        const OsGeom og = os_geom(KS, a.L.RB(), a.src.base1 != nullptr);
+        if (og.wr && og.rpw == 2)
+            return os_launch<KS, 8, 2>(a, wfull, S, st);
+        if (og.wr)
+            return os_launch<KS, 8, 1>(a, wfull, S, st);
+    } else if constexpr (KS == 24) {
+        if (os_geom(KS, a.L.RB(), a.src.base1 != nullptr).wr)
             return os_launch<KS, 8, 1>(a, wfull, S, st);
     }
     constexpr int NSTS = KS == 1 ? 16 : 8;
@@ -2802,7 +2824,7 @@ std::string matrix_kernel_names(const MatLayout& L, long long words, bool in_oor
             nst = 4;
             rsplit = true;
         }
-        const OsGeom og = os_geom(KS, RB);
+        const OsGeom og = os_geom(KS, RB, two);
         if (og.wr)
             r = "matrix_os_kernel<" + std::to_string(KS) + ", " + std::to_string(og.wr) + ", " +
                 std::to_string(og.rpw) + ", " + tf(two) + ">";
