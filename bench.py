@@ -256,7 +256,7 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--stripes", type=int, default=None)
     ap.add_argument("--cfg", choices=sorted(CONFIGS), default="cfg2")
     ap.add_argument("--systematic", action="store_true")
@@ -491,10 +491,13 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
     # tools/ramp.py)
     # the kernel times come from HIP events on the last n_ev warmup steps,
     # which run back to back into the timed region: event markers between
-    # the kernels of a timed step added launch bubbles to the wall time
-    # (--timed-events: on the timed steps instead, as before)
-    # (not the first warmup step, which is followed by the host-side check)
-    n_ev = 0 if timed_events else min(10, warmup - 1 if warmup > 1 else warmup)
+    # the kernels of a timed step added launch bubbles to the wall time.
+    # With few warmup steps those would follow the host-side check too
+    # closely (the clock drops while the GPU idles: cfg2 encode 3.94 vs
+    # 3.45 ms on warmup steps 1-2), so then the events go on the last
+    # n_tev timed steps instead (--timed-events: on every timed step)
+    n_ev = 0 if timed_events or warmup < 12 else min(8, warmup - 4)
+    n_tev = steps if timed_events else (0 if n_ev else min(5, steps))
     ok = True
     for w in range(warmup):
         step(w >= warmup - n_ev)
@@ -507,8 +510,8 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step(n_ev == 0)
+    for i in range(steps):
+        step(i >= steps - n_tev)
     sync()
     if dist:
         dist.barrier()
@@ -533,9 +536,10 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
     else:
         kernels = plan.kernels(P)
     return {"ctx_overlap": overlap, "events_on": (
-                "timed steps" if n_ev == 0 else
                 f"warmup steps {warmup - n_ev}..{warmup - 1} (back to back into "
-                f"the timed region, which runs without event markers)"),
+                f"the timed region, which runs without event markers)" if n_ev else
+                "every timed step" if n_tev == steps else
+                f"the last {n_tev} of the {steps} timed steps"),
             "k": k, "m": m, "n": n, "P": P, "pkt_bytes": pkt_bytes, "S": S,
             "C": C, "NC": NC, "sys": sys_, "steps": steps, "elapsed": elapsed,
             "ok": ok, "enc_ms": enc_ms, "dec_ms": dec_ms, "ctx_ms": ctx_ms,
