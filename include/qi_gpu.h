@@ -103,8 +103,9 @@ size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
  * multiple of 1024 columns (then followed by the NTT engine's context, used
  * when the decode's rows are not addressable by the matrix cores); the NTT
  * decode's per-pattern constants (src/fec_context.h:232-274, whose decode
- * reads the OOR buckets directly) otherwise.  h_ids is unused (kept for ABI
- * stability; may be NULL). */
+ * reads the OOR buckets directly) otherwise; for 256 < k <= 384 the NTT
+ * engine's half is built by the first decode that needs it.  h_ids is
+ * unused (kept for ABI stability; may be NULL). */
 int qi_gpu_decode_ctx(qi_plan* plan, const uint16_t* d_ids,
                       const uint16_t* h_ids, int n_stripes,
                       const uint32_t* d_oor_counts,
@@ -116,7 +117,13 @@ int qi_gpu_decode_ctx(qi_plan* plan, const uint16_t* d_ids,
  *   otherwise (coded row / parity): d_coded + s*css + slot*crs
  * with slot = f - k (systematic) or f (non-systematic).
  * OOR buckets of the coded rows are indexed by the same slot (slots =
- * n_outputs); pass NULL counts when there are none.  Output: k data rows. */
+ * n_outputs); pass NULL counts when there are none.  Output: k data rows.
+ * The context is not const in effect: a decode whose rows the matrix cores
+ * cannot address fills the context's lazily built sections (the dot2
+ * kernel's packed rows for k <= 256, the NTT engine's half for 256 < k <=
+ * 384) the first time, on `stream`, and records that in the context.  So a
+ * context may serve any number of decodes on one stream, but must not be
+ * used by decodes on two streams at once. */
 int qi_gpu_decode(qi_plan* plan, const void* d_ctx, const uint16_t* d_ids,
                   const uint16_t* d_data, long long dss, long long drs,
                   const uint16_t* d_coded, long long css, long long crs,
