@@ -2574,11 +2574,12 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
         return -2;
     const uint64_t bit = dev < 64 ? 1ull << dev : 0;
     if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
+        // (two source regions only at RPW = 1, os_geom)
         if (lds > 65536 &&
-            (hipFuncSetAttribute(
-                 reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, true>),
-                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) !=
-                 hipSuccess ||
+            ((RPW == 1 && hipFuncSetAttribute(
+                              reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, 1, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds)) != hipSuccess) ||
              hipFuncSetAttribute(
                  reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, false>),
                  hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2633,11 +2634,14 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
     if (blocks > 0x7fffffffLL)
         return -1;
     a.tiles = static_cast<int>(TS);
-    if (a.src.base1)
-        hipLaunchKernelGGL((matrix_os_kernel<KS, WR, RPW, true>),
-                           dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), lds, st,
-                           a, G, static_cast<int>(C), static_cast<int>(TS));
-    else
+    if (a.src.base1) {
+        if constexpr (RPW != 1)
+            return -1;  // not chosen by os_geom
+        else
+            hipLaunchKernelGGL((matrix_os_kernel<KS, WR, 1, true>),
+                               dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), lds, st,
+                               a, G, static_cast<int>(C), static_cast<int>(TS));
+    } else
         hipLaunchKernelGGL((matrix_os_kernel<KS, WR, RPW, false>),
                            dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), lds, st,
                            a, G, static_cast<int>(C), static_cast<int>(TS));
@@ -2653,14 +2657,15 @@ inline OsGeom os_geom(int KS, int RB, bool two)
 {
     if (!kMmOs)
         return {0, 0};
-    // KS = 16, 20 with more than one block of 8 row blocks, one source
+    // KS = 16, 20, 24 with more than one block of 8 row blocks, one source
     // region: two row blocks per wave, so one group (k200, k256) or two
-    // (k300) stage each input tile instead of two or three (k200 decode
-    // 0.757 -> 0.66 ms, k300 0.704 -> 0.653, k256 0.30 -> 0.278; encodes
-    // 10 % faster).  Not at KS = 24 (256 VGPRs and scratch), nor for the
-    // systematic decodes' two regions (k300 sys decode 1.05 -> 1.41 ms), nor
-    // at KS = 8 (k128 encode 0.725 -> 0.757 ms; gpurun_out/ab_r5k)
-    if ((KS == 16 || KS == 20) && RB > 8 && !two)
+    // (k300, k384) stage each input tile instead of two or three (k200
+    // decode 0.757 -> 0.66 ms, k300 0.704 -> 0.653, k256 0.30 -> 0.278,
+    // k384 0.88 -> 0.83; encodes ~10 % faster).  Not for the systematic
+    // decodes' two regions (k300 sys decode 1.05 -> 1.41 ms; at KS = 24 that
+    // variant spills), nor at KS = 8 (k128 encode 0.725 -> 0.757 ms;
+    // gpurun_out/ab_r5k, ab_r5l)
+    if ((KS == 16 || KS == 20 || KS == 24) && RB > 8 && !two)
         return {8, 2};
     if (KS >= 8)
         return {8, 1};
@@ -2685,14 +2690,11 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
     } else if constexpr (KS == 8) {
         if (os_geom(KS, a.L.RB(), a.src.base1 != nullptr).wr)
             return os_launch<KS, 8, 1>(a, wfull, S, st);
-    } else if constexpr (KS == 16 || KS == 20) {
+    } else if constexpr (KS == 16 || KS == 20 || KS == 24) {
         const OsGeom og = os_geom(KS, a.L.RB(), a.src.base1 != nullptr);
         if (og.wr && og.rpw == 2)
             return os_launch<KS, 8, 2>(a, wfull, S, st);
         if (og.wr)
-            return os_launch<KS, 8, 1>(a, wfull, S, st);
-    } else if constexpr (KS == 24) {
-        if (os_geom(KS, a.L.RB(), a.src.base1 != nullptr).wr)
             return os_launch<KS, 8, 1>(a, wfull, S, st);
     }
     constexpr int NSTS = KS == 1 ? 16 : 8;
