@@ -484,6 +484,18 @@ def test_cfg3_random_patterns_vs_oracle():
                      windows=[(0, 256), (1024 - 128, 1024 + 128), (P - 256, P)])
 
 
+def test_cfg3_full_batch_vs_oracle():
+    """BASELINE configs[2] at its full bench size: 1024 stripes of k=64,
+    n=1024, 4 KiB packets, each decoded from its own random 64-subset (the
+    bench's batch checks only the round trip); every stripe round-trips, and
+    stripes 0, 32, 64, ..., 1023 match the oracle by column windows
+    (outputs, OOR lists, decodes)."""
+    P = 2048
+    _batch_roundtrip(64, 960, 0, 1024, P, seed=7, n_craft=0, check_oracle=False,
+                     oracle_stripes=_spread(1024, 32),
+                     windows=[(0, 128), (1024 - 64, 1024 + 64), (P - 128, P)])
+
+
 @pytest.mark.parametrize("k,m,S,P", [
     (16, 48, 4096, 256),    # ~0.1 % of the stripes need a row scale
     (64, 960, 96, 1024),    # ~27 %
