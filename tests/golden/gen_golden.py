@@ -183,6 +183,96 @@ def _gen_cabi(ref, ora, name, k, m, sys_, block_bytes, seed, n_patterns,
     print(f"{name}: C-ABI k={k} m={m} sys={sys_} block={block_bytes} md={md}")
 
 
+def all_patterns(k, m):
+    """Every decodable erasure set of a (k, m) code, 0 .. m missing, in the
+    order of test/quadiron_c_utest.cpp:58-74,283-295 (combinations of
+    size i = 0..m, lexicographic, from prev_permutation over a selector with
+    the first i entries set)."""
+    import itertools
+    return [list(c) for i in range(m + 1)
+            for c in itertools.combinations(range(k + m), i)]
+
+
+def _gen_cabi_scn(ref, ora, name, k, m, sys_, block_bytes, seed, patterns,
+                  n_craft, out_dir):
+    """C-ABI scenario fixtures: the reference's own C-ABI test sequence,
+    test_encode_decode_reconstruct (test/quadiron_c_utest.cpp:109-281), run
+    through oracle/_ref for every given erasure pattern:
+
+      encode (all outputs wanted) -> zero the missing fragments -> decode ->
+      (non-sys: put the k coded fragments back) -> zero the missing fragments
+      -> reconstruct every missing data index, then every missing parity
+      index, in ascending order, on the SAME buffers (so later reconstructs
+      see the earlier ones' results in buffers still flagged missing).
+
+    Stored: the encoded fragments; per pattern the decoded fragments' FNT1
+    headers, and per reconstruct (rec_pat / rec_dest) the reconstructed
+    fragment's FNT1 header.  Payloads are not stored twice: the reference's
+    outputs are asserted here to be the input data (decode; systematic data
+    reconstruct) or the encoded fragment, header included (every other
+    reconstruct), exactly the reference test's own checks."""
+    rng = np.random.default_rng(seed)
+    codec = Codec()
+    assert ora.qo_codec_init(C.byref(codec), k, m, sys_) == 0
+    md = ref.ref_metadata_size(C.c_size_t(block_bytes))
+    L = md + block_bytes
+    payload = rng.integers(0, 256, (k, block_bytes), dtype=np.uint8)
+    if n_craft:
+        craft_oor(ora, codec, payload, rng, n_craft)
+    data = np.zeros((k, L), np.uint8)
+    data[:, md:] = payload
+    d = [data[i].copy() for i in range(k)]
+    p = [np.zeros(L, np.uint8) for _ in range(m)]
+    wanted = np.ones(codec.n_outputs, np.int32)
+    assert ref.ref_c_encode(sys_, k, m, ptrs(d), ptrs(p), vp(wanted),
+                            C.c_size_t(block_bytes)) == 0
+    enc_data, enc_par = np.stack(d), np.stack(p)
+    missing = np.zeros((len(patterns), k + m), np.int32)
+    dec_hdr = np.zeros((len(patterns), k, md), np.uint8)
+    rec_pat, rec_dest, rec_hdr = [], [], []
+    for t, miss in enumerate(patterns):
+        missing[t, miss] = 1
+        mv = missing[t]
+        D = [enc_data[i].copy() for i in range(k)]
+        P = [enc_par[i].copy() for i in range(m)]
+        for i in miss:
+            (D + P)[i][:] = 0
+        assert ref.ref_c_decode(sys_, k, m, ptrs(D), ptrs(P), vp(mv),
+                                C.c_size_t(block_bytes)) == 0
+        for i in range(k):
+            assert (D[i][md:] == payload[i]).all(), (name, miss, i)
+            dec_hdr[t, i] = D[i][:md]
+        if not sys_:
+            D = [enc_data[i].copy() for i in range(k)]
+        for i in miss:
+            (D + P)[i][:] = 0
+        for dest in sorted(miss):
+            assert ref.ref_c_reconstruct(sys_, k, m, ptrs(D), ptrs(P), vp(mv),
+                                         C.c_uint(dest),
+                                         C.c_size_t(block_bytes)) == 0
+            got = (D + P)[dest]
+            # the reference test's own checks (quadiron_c_utest.cpp:241-276)
+            if dest < k and sys_:
+                assert (got[md:] == payload[dest]).all()
+            else:
+                exp = (enc_par[dest - k] if dest >= k
+                       else enc_data[dest])
+                assert (got == exp).all(), (name, miss, dest)
+            rec_pat.append(t)
+            rec_dest.append(dest)
+            rec_hdr.append(got[:md].copy())
+    rec_hdr = np.stack(rec_hdr) if rec_hdr else np.zeros((0, md), np.uint8)
+    np.savez_compressed(
+        os.path.join(out_dir, name + ".npz"),
+        params=np.array([k, m, sys_, block_bytes, md], np.int64),
+        data=data, enc_data=enc_data, enc_parity=enc_par, missing=missing,
+        decoded_hdr=dec_hdr, rec_pat=np.array(rec_pat, np.int32),
+        rec_dest=np.array(rec_dest, np.int32), rec_hdr=rec_hdr)
+    print(f"{name}: C-ABI scenarios k={k} m={m} sys={sys_} "
+          f"block={block_bytes} patterns={len(patterns)} "
+          f"reconstructs={len(rec_dest)}")
+
+
 def main():
     if not os.path.exists(REF):
         sys.exit("build the reference first: make -C oracle ref")
@@ -248,6 +338,25 @@ def main():
     gen_blocks(ref, ora, "blk_k1000_m24", 1000, 24, 0, 64, 256 + 6, 45, 2, 8, out)
     gen_blocks(ref, ora, "blk_k500_m12_sys", 500, 12, 1, 128, 512, 46, 2, 8, out)
     gen_blocks(ref, ora, "blk_k2000_m48", 2000, 48, 0, 32, 128 + 2, 47, 2, 8, out)
+
+    def gen_scn(*a):
+        if not only or a[2] in only:
+            _gen_cabi_scn(*a)
+    # the reference's exhaustive C-ABI scenario test (round 6):
+    # test/quadiron_c_utest.cpp:283-309 -- (3, 3), block 10000, every
+    # 0..m-erasure pattern (42 per type), every missing index reconstructed
+    gen_scn(ref, ora, "cabiscn_k3_m3", 3, 3, 0, 10000, 51,
+            all_patterns(3, 3), 4, out)
+    gen_scn(ref, ora, "cabiscn_k3_m3_sys", 3, 3, 1, 10000, 52,
+            all_patterns(3, 3), 4, out)
+    # cfg2-shaped (16, 48) at a 64 KiB + 2 block: fewer-than-m erasures, so
+    # the decoder's first-k choice (src/fec_base.h:1199-1236) is exercised,
+    # with data and parity fragments missing together
+    cfg2_pats = [[], [3], [0, 17, 40], [1, 2, 5, 15, 16, 33, 63],
+                 list(range(0, 32, 2)) + [47, 50],
+                 [i for i in range(64) if i % 4 != 1][:47]]
+    gen_scn(ref, ora, "cabiscn_k16_m48", 16, 48, 0, 65536 + 2, 53,
+            cfg2_pats, 24, out)
 
 
 if __name__ == "__main__":

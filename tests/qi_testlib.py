@@ -67,6 +67,53 @@ def golden_names(prefix):
                   for p in glob.glob(os.path.join(GOLDEN, prefix + "*.npz")))
 
 
+def check_cabi_scenarios(g, encode, decode, reconstruct):
+    """Replay a `cabiscn_*` fixture (tests/golden/gen_golden.py
+    `_gen_cabi_scn`): the reference's C-ABI test sequence
+    (test/quadiron_c_utest.cpp:109-281) for every stored erasure pattern,
+    through the given encode(D, P, wanted, B) / decode(D, P, miss, B) /
+    reconstruct(D, P, miss, dest, B) callables (the product's
+    quadiron_fnt32_* or the oracle's qo_fnt32_*), on the same mutated
+    buffers, comparing every fragment byte for byte: FNT1 headers against
+    the reference's, payloads against the data / encoded fragments the
+    reference produced."""
+    k, m, sys_, B, md = (int(v) for v in g["params"])
+    L = md + B
+    payload = g["data"][:, md:]
+    d = [g["data"][i].copy() for i in range(k)]
+    p = [np.zeros(L, np.uint8) for _ in range(m)]
+    wanted = np.ones(m if sys_ else k + m, np.int32)
+    assert encode(d, p, wanted, B) == 0
+    assert (np.stack(d) == g["enc_data"]).all()
+    assert (np.stack(p) == g["enc_parity"]).all()
+    enc = list(g["enc_data"]) + list(g["enc_parity"])
+    r = 0
+    for t in range(len(g["missing"])):
+        miss = np.ascontiguousarray(g["missing"][t], np.int32)
+        gone = np.flatnonzero(miss).tolist()
+        D = [g["enc_data"][i].copy() for i in range(k)]
+        P = [g["enc_parity"][i].copy() for i in range(m)]
+        for i in gone:
+            (D + P)[i][:] = 0
+        assert decode(D, P, miss, B) == 0, gone
+        for i in range(k):
+            assert (D[i][:md] == g["decoded_hdr"][t, i]).all(), (gone, i)
+            assert (D[i][md:] == payload[i]).all(), (gone, i)
+        if not sys_:
+            D = [g["enc_data"][i].copy() for i in range(k)]
+        for i in gone:
+            (D + P)[i][:] = 0
+        for dest in sorted(gone):
+            assert (g["rec_pat"][r], g["rec_dest"][r]) == (t, dest)
+            assert reconstruct(D, P, miss, dest, B) == 0, (gone, dest)
+            got = (D + P)[dest]
+            assert (got[:md] == g["rec_hdr"][r]).all(), (gone, dest)
+            exp = payload[dest] if (sys_ and dest < k) else enc[dest][md:]
+            assert (got[md:] == exp).all(), (gone, dest)
+            r += 1
+    assert r == len(g["rec_dest"])
+
+
 def oracle_encode_blocks(k, m, sys_, data, cap=None):
     """data: (k, B) uint8 -> outputs (n_outputs, B), oor (n_out, cap), cnt."""
     c = codec(k, m, sys_)

@@ -106,6 +106,27 @@ def test_cabi_vs_reference_golden(hip_lib, name):
         assert ((D + P)[dest] == g["reconstructed"][t]).all()
 
 
+@pytest.mark.parametrize("name", golden_names("cabiscn_"))
+def test_cabi_scenarios_vs_reference_golden(hip_lib, name):
+    """The reference's own exhaustive C-ABI test through quadiron_fnt32_*:
+    test/quadiron_c_utest.cpp:283-309 runs every 0..m erasure pattern of
+    (3, 3), systematic and not (42 patterns each), encode -> decode ->
+    reconstruct of EVERY missing fragment on the same buffers; plus a
+    cfg2-shaped (16, 48, 64 KiB + 2) fixture whose patterns miss fewer than
+    m fragments (the decoder's first-k choice, src/fec_base.h:1199-1236) and
+    reconstruct parities while data fragments are missing too
+    (src/quadiron_c.cpp:322-369).  Byte-for-byte, FNT1 headers included,
+    against the reference's outputs (tests/golden/gen_golden.py
+    `_gen_cabi_scn`)."""
+    import quadiron_amd as qa
+    from qi_testlib import check_cabi_scenarios
+    g = load(name)
+    k, m, sys_, B, md = (int(v) for v in g["params"])
+    h = qa.QuadironFnt32(2, k, m, sys_)
+    assert h.metadata_size(B) == md
+    check_cabi_scenarios(g, h.encode, h.decode, h.reconstruct)
+
+
 @pytest.mark.parametrize("k,m,sys_", [(4, 4, 0), (6, 3, 1)])
 def test_cabi_multi_chunk_block_vs_oracle(hip_lib, k, m, sys_):
     """quadiron_fnt32_encode / _decode on a block wider than one pipeline

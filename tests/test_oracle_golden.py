@@ -7,7 +7,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from qi_testlib import (Q, codec, golden_names, load, oracle,
+from qi_testlib import (Q, check_cabi_scenarios, codec, golden_names, load, oracle,
                         oracle_decode_blocks, oracle_encode_blocks,
                         oracle_nf4_decode_blocks, oracle_nf4_encode_blocks,
                         ptrs, vp)
@@ -116,6 +116,28 @@ def test_oracle_cabi_vs_reference(name):
         assert o.qo_fnt32_reconstruct(C.byref(c), ptrs(D), ptrs(P), vp(miss),
                                       C.c_uint(dest), C.c_size_t(B)) == 0
         assert ((D + P)[dest] == g["reconstructed"][t]).all()
+
+
+@pytest.mark.parametrize("name", golden_names("cabiscn_"))
+def test_oracle_cabi_scenarios_vs_reference(name):
+    """The reference's exhaustive C-ABI scenario test
+    (test/quadiron_c_utest.cpp:283-309: every 0..m erasure pattern of (3, 3),
+    every missing index reconstructed) and a cfg2-shaped (16, 48) fixture
+    with fewer-than-m erasures, replayed through the oracle's C glue."""
+    g = load(name)
+    k, m, sys_, B, md = (int(v) for v in g["params"])
+    c = codec(k, m, sys_)
+    o = oracle()
+    assert o.qo_metadata_size(C.c_size_t(B)) == md
+    check_cabi_scenarios(
+        g,
+        lambda D, P, w, B: o.qo_fnt32_encode(C.byref(c), ptrs(D), ptrs(P),
+                                             vp(w), C.c_size_t(B)),
+        lambda D, P, mi, B: o.qo_fnt32_decode(C.byref(c), ptrs(D), ptrs(P),
+                                              vp(mi), C.c_size_t(B)),
+        lambda D, P, mi, d, B: o.qo_fnt32_reconstruct(
+            C.byref(c), ptrs(D), ptrs(P), vp(mi), C.c_uint(d),
+            C.c_size_t(B)))
 
 
 @pytest.mark.parametrize("name", golden_names("nf4_"))
