@@ -97,14 +97,78 @@ def cpu_share():
         return os.cpu_count() or 1
 
 
+def _cpu_mhz():
+    """Current clock of every CPU in this process's affinity mask, from
+    /proc/cpuinfo ("cpu MHz" per processor), or [] where not readable."""
+    try:
+        mask = os.sched_getaffinity(0)
+    except AttributeError:
+        mask = None
+    out, proc = [], None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("processor"):
+                    proc = int(line.split(":", 1)[1])
+                elif line.startswith("cpu MHz") and (mask is None or proc in mask):
+                    out.append(float(line.split(":", 1)[1]))
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+class _HostSampler:
+    """Samples the host's clock and load while a CPU-baseline leg runs (the
+    leg is one ctypes call, which releases the GIL): the spread of the same
+    reference build across hosts (1-core legs from 0.2 to 3.3 GB/s) is read
+    against these."""
+
+    def __init__(self, period=0.25):
+        import threading
+        self.period, self.samples = period, []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self._stop.is_set():
+            mhz = _cpu_mhz()
+            if mhz:
+                self.samples.append(mhz)
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        self.load0 = os.getloadavg()
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join()
+        self.load1 = os.getloadavg()
+
+    def summary(self, threads):
+        allv = sorted(v for s in self.samples for v in s)
+        busiest = sorted(v for s in self.samples for v in sorted(s)[-threads:])
+        med = (lambda v: round(v[len(v) // 2], 1) if v else None)
+        return {"cpu_mhz_median_all": med(allv),
+                "cpu_mhz_median_busiest": med(busiest),
+                "cpu_mhz_max": round(allv[-1], 1) if allv else None,
+                "mhz_samples": len(self.samples),
+                "loadavg_1m_before_after": [round(self.load0[0], 2),
+                                            round(self.load1[0], 2)],
+                "pinning": f"none: {threads} std::thread(s) float over the "
+                           f"process's {len(_cpu_mhz()) or '?'} affinity CPUs"}
+
+
 def _ref_leg(lib, k, m, P, threads, seconds, systematic, missing):
     import ctypes as C
     enc_b, dec_b = alg_bytes(k, m, P, systematic)
     stripes = C.c_longlong()
     enc_s, dec_s = C.c_double(), C.c_double()
-    wall = lib.ref_bench(int(systematic), k, m, C.c_size_t(P), C.c_double(seconds),
-                         threads, missing.ctypes.data_as(C.c_void_p),
-                         C.byref(stripes), C.byref(enc_s), C.byref(dec_s))
+    with _HostSampler() as hs:
+        wall = lib.ref_bench(int(systematic), k, m, C.c_size_t(P), C.c_double(seconds),
+                             threads, missing.ctypes.data_as(C.c_void_p),
+                             C.byref(stripes), C.byref(enc_s), C.byref(dec_s))
     n = stripes.value
     # thread-time per stripe in each phase (the decode's share includes
     # building its DecodeContext, src/fec_base.h:1177-1321)
@@ -114,7 +178,8 @@ def _ref_leg(lib, k, m, P, threads, seconds, systematic, missing):
             "encode_ms_per_stripe": round(enc_ms, 4),
             "decode_ms_per_stripe": round(dec_ms, 4),
             "encode_GBps_per_thread": round(enc_b / enc_ms / 1e6, 3),
-            "decode_GBps_per_thread": round(dec_b / dec_ms / 1e6, 3)}
+            "decode_GBps_per_thread": round(dec_b / dec_ms / 1e6, 3),
+            "host": hs.summary(threads)}
 
 
 def _port_leg(k, m, P, seconds, systematic, missing):
@@ -608,8 +673,16 @@ def report(res, cfg, world, steps, warmup, dry):
             return {}
         same = bool(build and rp.get("build") and
                     build.split("+src:")[-1] == rp["build"].split("+src:")[-1])
+        # frac_rocprof: the kernel trace over the profiled run's timed steps;
+        # frac_stats: the --stats summary average over every call (warmup
+        # steps at a ramping clock included), the lowest of the three
+        allc = r.get("avg_ms_all_calls")
         return {"frac_rocprof": nbytes / (r["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "rocprof_ms": r["avg_ms"], "rocprof_source": rp.get("source"),
+                "rocprof_ms": r["avg_ms"],
+                "frac_stats": (nbytes / (allc * 1e-3) / 1e9 / HBM_PEAK_GBS
+                               if allc else None),
+                "stats_ms": allc,
+                "rocprof_source": rp.get("source"),
                 "rocprof_same_build": same}
 
     out = {

@@ -155,8 +155,9 @@ int qi_gpu_decode_packed(qi_plan* plan, const void* d_ctx,
  * marks than its capacity (oor_cap), i.e. some out-of-range symbols could
  * not be restored and the affected stripes are wrong (bit 1), or if a decode
  * context was built from ids that were not distinct or not below n (bit 2;
- * checked where the context derives the erased set from the ids: the
- * erasure decode of k > 384, n - k <= 64).  Sticky per plan; reset by
+ * every context builder checks: a repeated id makes A'(x_i) = 0, and the
+ * erasure decode of k > 384, n - k <= 64, derives its erased set from the
+ * ids).  Sticky per plan; reset by
  * reading.  Synchronous.  Tiles with many marks need no capacity of their
  * own: they are decoded by a slower path, never refused. */
 int qi_gpu_take_error(qi_plan* plan);

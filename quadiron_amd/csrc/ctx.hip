@@ -392,7 +392,7 @@ __host__ __device__ inline int ctx_pitch(int k)
 
 template <int NT, bool BIG>
 __global__ __launch_bounds__(NT) void decode_ctx_kernel(
-    int k, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
+    int k, int n, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
     int32_t* __restrict__ ctx, long long ctx_stride, Oor in_oor, int slot_base,
     int by_pos, long long words, int dot2, uint32_t* err, int nb)
 {
@@ -443,14 +443,23 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     if (tid < k) {
         const uint32_t id = ids[static_cast<long long>(s) * k + tid];
         xs[tid] = powm(r, id);
-        if (lead)
+        if (lead) {
             cids[tid] = static_cast<int32_t>(id);
+            if (id >= static_cast<uint32_t>(n))  // not a point of the code
+                atomicOr(err, kErrBadIds);
+        }
     }
+    // the route-table clears (every thread of the lead block, above) must
+    // have reached memory before any thread's atomicAdd below: each wave
+    // waits for its own stores, then the barrier
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (lead && in_oor.counts && tid < k) {
         const int id = ids[static_cast<long long>(s) * k + tid];
         const int slot = (by_pos ? tid : id) - slot_base;
-        if (slot >= 0) {
+        // rows outside the bucket array (systematic data rows below
+        // slot_base; bad ids past it) have no marks here
+        if (slot >= 0 && slot < in_oor.slots) {
             const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
             uint32_t c = in_oor.counts[bk];
             if (c > static_cast<uint32_t>(in_oor.cap)) {
@@ -648,6 +657,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             const uint32_t ap = canon_lz(fold(h));
             aprime[tid] = ap;
             cinv[tid] = inv_lz(ap);
+            if (ap == 0u)  // x_i = x_j for some j != i: repeated ids
+                atomicOr(err, kErrBadIds);
         }
     } else if (tid < k) {
         // Q_i = A / (x - x_i) by synthetic division from the top, and
@@ -669,6 +680,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         const uint32_t ap = canon_lz(fold(h));
         aprime[tid] = ap;
         cinv[tid] = inv_lz(ap);
+        if (ap == 0u)  // repeated ids
+            atomicOr(err, kErrBadIds);
     }
     if (mode != 0) {
         // systematic: M[t][i] = Q_i(r^t) / A'(x_i), one thread per row t,
@@ -920,6 +933,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         xt = balanced(canon_lz(rpow_lz(rp, id, lgn)));
         xs[tid] = static_cast<uint32_t>(xt < 0 ? xt + kQ : xt);
         cids[tid] = static_cast<int32_t>(id);
+        if (id >= (1u << lgn))  // not a point of the code
+            atomicOr(err, kErrBadIds);
     }
     if (tid < 64 && 64 + tid < k)
         xt1 = balanced(canon_lz(rpow_lz(rp, ids[static_cast<long long>(s) * k + 64 + tid], lgn)));
@@ -961,7 +976,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         for (int i = rl; i < k; i += 64) {
             const int id = ids[static_cast<long long>(s) * k + i];
             const int slot = (by_pos ? i : id) - slot_base;
-            if (slot < 0)
+            if (slot < 0 || slot >= in_oor.slots)
                 continue;
             const long long bk = static_cast<long long>(s) * in_oor.slots + slot;
             uint32_t c = in_oor.counts[bk];
@@ -1043,6 +1058,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         const uint32_t ap = canon_lz(fold(h));
         aprime[tid] = ap;
         cinv[tid] = inv_lz(ap);
+        if (ap == 0u)  // repeated ids
+            atomicOr(err, kErrBadIds);
     }
     if (mode != 0) {
         // systematic: M[t][i] = Q_i(r^t) / A'(x_i), one thread per row t,
@@ -1328,7 +1345,7 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
         if (static_cast<long long>(S) * nb > 0x7fffffffLL)
             return -1;
         hipLaunchKernelGGL((decode_ctx_kernel<1024, true>), dim3(S * nb), dim3(1024), lds, st, k,
-                           r, mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
+                           n, r, mode, L, d_ids, d_ctx, ctx_stride, in_oor ? *in_oor : none,
                            slot_base, by_pos, words, dot2, err, nb);
         return hipGetLastError() == hipSuccess ? 0 : -2;
     }

@@ -590,10 +590,15 @@ constexpr int kRedoCols = 64;
 // that holds a mark (all marks of the column restored, plain canonical
 // arithmetic) and store it again: NT threads, LDS scratch xs (kin x
 // kRedoCols u16), mk (kin x kRedoCols / 32 u32), colmk (kRedoCols / 32 u32).
-// The caller has waited for its own stores of these columns.
+// The caller has waited for its own stores of these columns.  Only the
+// output rows of row blocks gq, gq + G, gq + 2G, ... (16 rows each) are
+// recomputed: a block of matrix_os_kernel redoes just the rows it stored
+// itself (G row-block groups share a column range), so no two blocks write
+// the same outputs; other callers pass gq = 0, G = 1 (every row).
 template <int NT>
 __device__ void redo_columns(const MatArgs& a, int s, long long t0c, long long t1c,
-                             uint16_t* xs, uint32_t* mk, uint32_t* colmk)
+                             uint16_t* xs, uint32_t* mk, uint32_t* colmk, int gq = 0,
+                             int G = 1)
 {
     const MatLayout L = a.L;
     const int kin = L.kin;
@@ -638,7 +643,11 @@ __device__ void redo_columns(const MatArgs& a, int s, long long t0c, long long t
         }
         __syncthreads();
         if ((colmk[c / 32] >> (c % 32)) & 1u) {
-            for (int t = wv; t < L.R; t += NT / 64) {
+            const int nrows = 16 * ((L.RB() - gq + G - 1) / G);
+            for (int it = wv; it < nrows; it += NT / 64) {
+                const int t = 16 * (gq + G * (it >> 4)) + (it & 15);
+                if (t >= L.R)
+                    continue;
                 uint64_t acc = 0;
                 for (int j = 0; j < kin; j++) {
                     const uint32_t x = (mk[j * (kRedoCols / 32) + c / 32] >> (c % 32)) & 1u
@@ -2080,9 +2089,12 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
                 const int tile = t0 + 32 * wd + __builtin_ctz(bits);
                 bits &= bits - 1;
                 const long long c0 = static_cast<long long>(tile) * NCOL;
+                // this group's row blocks only: the G blocks of a column
+                // range each redo (and earlier stored) disjoint rows
                 redo_columns<512>(a, s, c0, c0 + NCOL, reinterpret_cast<uint16_t*>(qi_lds),
                                   reinterpret_cast<uint32_t*>(qi_lds + kin * 2 * kRedoCols),
-                                  reinterpret_cast<uint32_t*>(qi_lds + kin * (2 * kRedoCols + 8)));
+                                  reinterpret_cast<uint32_t*>(qi_lds + kin * (2 * kRedoCols + 8)),
+                                  gq, G);
             }
         }
     };

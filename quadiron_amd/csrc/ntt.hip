@@ -266,6 +266,7 @@ __device__ __forceinline__ uint32_t mulm24(uint32_t a, uint32_t b)
 }
 
 constexpr int kCtxChains = 4;  // independent product chains per thread
+constexpr int kPosChunk = 2048;  // posmap positions staged in LDS per pass
 
 // The per-pattern constants as independent products, one item per thread
 // (DecodeContext::init, src/fec_context.h:232-274, restated):
@@ -299,20 +300,34 @@ __global__ __launch_bounds__(kNttBlock) void ntt_ctx_kernel(NttCtxArgs a)
     for (int i = tid; i < kp; i += kNttBlock)
         xs[i] = i < k ? powm_(a.r, id_of(i)) : 0xffffffffu;
     if (blockIdx.y == 0) {
-        for (int t = tid; t < a.L.n; t += kNttBlock)
-            posmap[t] = -1;
-    }
-    __syncthreads();
-    if (blockIdx.y == 0) {
+        // posmap[t] = the received row holding sequence element t, or -1.
+        // Every global word is written once with its final value (staged in
+        // LDS, kPosChunk positions at a time): a lazy rebuild racing with a
+        // decode on another stream that reads the same context
+        // only ever rewrites a word with the value it already holds.
+        __shared__ int32_t pm[kPosChunk];
         for (int i = tid; i < k; i += kNttBlock) {
             const int id = static_cast<int>(id_of(i));
             ids[i] = id;
-            if (id < a.L.n)
-                posmap[id] = i;
-            else
+            if (id >= a.L.n)
                 atomicOr(a.err, kErrBadIds);
         }
+        for (int c0 = 0; c0 < a.L.n; c0 += kPosChunk) {
+            for (int t = tid; t < kPosChunk; t += kNttBlock)
+                pm[t] = -1;
+            __syncthreads();
+            for (int i = tid; i < k; i += kNttBlock) {
+                const int id = static_cast<int>(id_of(i));
+                if (id >= c0 && id < c0 + kPosChunk)
+                    pm[id - c0] = i;
+            }
+            __syncthreads();
+            for (int t = tid; t < kPosChunk && c0 + t < a.L.n; t += kNttBlock)
+                posmap[c0 + t] = pm[t];
+            __syncthreads();
+        }
     }
+    __syncthreads();
     const int u = blockIdx.y * kNttBlock + tid;
     const int len2k = a.L.len2k;
     if (u >= len2k + k)
@@ -337,8 +352,11 @@ __global__ __launch_bounds__(kNttBlock) void ntt_ctx_kernel(NttCtxArgs a)
     uint32_t p = mulm24(mulm24(acc[0], acc[1]), mulm24(acc[2], acc[3]));
     if (is_c)
         C[u] = static_cast<int32_t>(subm_(0u, mulm24(p, a.inv_len2k)));
-    else
+    else {
         invA[self] = static_cast<int32_t>(powm_(mulm24(p, z), 65535u));
+        if (p == 0u)  // A'(x_i) = 0: x_i = x_j for some j != i (repeated ids)
+            atomicOr(a.err, kErrBadIds);
+    }
 }
 
 // after a lazy ntt_ctx_kernel launch on the same stream: mark the stripes'

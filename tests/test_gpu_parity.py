@@ -611,6 +611,46 @@ def test_unaligned_rows_whole_tiles(k, m, sys_):
     assert torch.equal(dec, dd)
 
 
+def test_lazy_ntt_ctx_two_streams():
+    """256 < k <= 384 at whole tiles: the context holds the matrix form, and
+    the NTT engine's half is built by the first decode whose rows the matrix
+    cores cannot address.  Two such decodes from ONE context on two streams
+    at once may both find that half unbuilt and both build it; every word of
+    it is written once with its final value (no transient -1 in the position
+    map), so both decodes come out right.  Repeated over fresh
+    contexts (each rebuild clears the lazy word)."""
+    torch = _torch()
+    import quadiron_amd as qa
+    k, m, S, P = 300, 212, 4, 1024
+    plan = qa.Plan(k, m, False)
+    rng = np.random.default_rng(23)
+    data = rng.integers(0, 65536, (S, k, P), dtype=np.uint16)
+    dd = torch.from_numpy(data.view(np.int16)).cuda()
+    obig = torch.zeros((S, plan.n_outputs, P + 1), dtype=torch.int16, device="cuda")
+    out = obig[:, :, 1:]  # rows at odd u16 offsets: the NTT engine decodes
+    cap = 64
+    counts = torch.zeros(S * plan.n_outputs, dtype=torch.int32, device="cuda")
+    entries = torch.zeros(S * plan.n_outputs * cap, dtype=torch.int32, device="cuda")
+    plan.encode(dd, out, counts, entries, cap)
+    ctx = torch.zeros(plan.ctx_bytes(S, P), dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for rep in range(4):
+        ids = np.stack([np.sort(rng.choice(k + m, k, replace=False))
+                        for _ in range(S)]).astype(np.uint16)
+        di = torch.from_numpy(ids.view(np.int16)).cuda()
+        plan.decode_ctx(di, ctx, P, counts, entries, cap)
+        torch.cuda.synchronize()
+        decs = [torch.zeros((S, k, P + 1), dtype=torch.int16, device="cuda")[:, :, 1:]
+                for _ in range(2)]
+        for st, dec in zip((s1, s2), decs):
+            assert plan.decode(ctx, di, out, dec, counts=counts, entries=entries,
+                               cap=cap, stream=st.cuda_stream, check=False) == 0
+        torch.cuda.synchronize()
+        assert plan.take_error() == 0
+        for dec in decs:
+            assert torch.equal(dec, dd), rep
+
+
 def test_big_matrix_ctx_sized_for_a_wider_batch():
     """A context buffer sized for the widest batch (ragged: NTT format) holds
     the contexts of a narrower whole-tile batch (matrix format, larger): the
@@ -819,25 +859,33 @@ def test_decode_bucket_overflow_raises(k, m):
 
 
 @pytest.mark.parametrize("bad", ["repeated", "past_n"])
-def test_erasure_ctx_bad_ids_raise(bad):
-    """The erasure decode's context (k > 384, n - k <= 64) derives the erased
-    set from the received ids.  A repeated id (more than n - k positions
-    then look erased) or an id >= n must raise the plan's sticky error and
-    write nothing outside the stripe's own context: the next stripe's
-    context is the one it builds alone, and guard bytes behind the buffer
-    stay untouched."""
+@pytest.mark.parametrize("k,m,n,P,kern", [
+    (500, 10, 512, 64, "ntt_eras_kernel"),          # erasure context
+    (16, 48, 64, 64, "decode_ctx_lds_kernel<128>"),  # matrix contexts
+    (64, 960, 1024, 1024, "decode_ctx_lds_kernel<256>"),
+    (200, 56, 256, 1024, "decode_ctx_kernel<1024, true>"),
+    (300, 212, 512, 1024, "decode_ctx_kernel<1024, true>"),
+    (600, 1400, 2048, 256, "ntt_ctx_kernel"),       # the general NTT decode
+])
+def test_ctx_bad_ids_raise(bad, k, m, n, P, kern):
+    """Every decode-context builder checks the received ids: a repeated id
+    (two equal points: A'(x_i) = 0, or more than n - k positions looking
+    erased) or an id >= n must raise the plan's sticky error and write
+    nothing outside the stripe's own context: the next stripe's context is
+    the one it builds alone, and guard bytes behind the buffer stay
+    untouched (the erasure context; r5: the matrix contexts)."""
     torch = _torch()
     import quadiron_amd as qa
-    k, m, S, P = 500, 10, 2, 64
+    S = 2
     plan = qa.Plan(k, m, False)
-    assert "ntt_eras_kernel" in plan.kernels(P)
+    assert kern in plan.kernels(P)
     rng = np.random.default_rng(3)
     ids = np.stack([np.sort(rng.choice(k + m, k, replace=False))
                     for _ in range(S)]).astype(np.uint16)
     if bad == "repeated":
         ids[0, 7] = ids[0, 6]
     else:
-        ids[0, -1] = 600  # n = 512
+        ids[0, -1] = n + 88
     di = torch.from_numpy(ids.view(np.int16)).cuda()
     nb = plan.ctx_bytes(S, P)
     cs = plan.ctx_bytes(1, P)
