@@ -95,6 +95,46 @@ __global__ __launch_bounds__(256) void fill_rows(char* base, size_t stripe_bytes
     }
 }
 
+// the cfg3 generator encode's store ORDER without its loads or math
+// (1024 stripes x 1024 rows x 4 KiB): block = (stripe, column tile of CT
+// columns), 4 waves, wave w walks row blocks w, w + 4, ... (16 rows each);
+//   MODE 0: per 64-column super tile two store instructions of 8 rows x
+//           128 B (the product's LDS-transposed epilogue, gen_mfma_kernel)
+//   MODE 1: per row of the row block, CT * 2 bytes as 1 KiB instructions
+//           (each instruction one contiguous run of one row)
+template <int AUX, int CT, int MODE, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void fill_tiles(char* base, int S)
+{
+    constexpr int NT = 2048 / CT;  // column tiles per stripe
+    const int b = blockIdx.x, x = b & 7, j = b >> 3;
+    const int grp = j / NT, ct = j - grp * NT;
+    const int s = grp * 8 + x;
+    if (s >= S)
+        return;
+    __amdgpu_buffer_rsrc_t r = rsrc(base + static_cast<size_t>(s) * (1024u * 4096u),
+                                    1024u * 4096u);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const v4i v = {l, s, ct, 9};
+    const unsigned c0 = ct * CT * 2;
+    for (int rb = w; rb < 64; rb += NW) {
+        if constexpr (MODE == 0) {
+#pragma unroll
+            for (int st = 0; st < CT / 64; st++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int row = 16 * rb + 8 * h + (l >> 3);
+                    st16<AUX>(r, row * 4096u + c0 + st * 128 + 16 * (l & 7), v);
+                }
+        } else {
+#pragma unroll
+            for (int rr = 0; rr < 16; rr++)
+#pragma unroll
+                for (int q = 0; q < CT * 2 / 1024; q++)
+                    st16<AUX>(r, (16 * rb + rr) * 4096u + c0 + q * 1024 + 16 * l, v);
+        }
+    }
+}
+
 // the encode's memory shape without math: read K rows of a stripe's data
 // (RB bytes each), write N rows (RB bytes each); one block per (stripe,
 // 4 KiB column piece), the block's loads first, then its stores
@@ -159,6 +199,36 @@ int main()
     rep("fill stripe 64KiB pieces " NAME " " #SB, SB * S, timeit([&] {                         \
             fill_stripe<AUX, 65536><<<S * (SB / 65536), 256>>>(out, SB, S);                     \
         }, 10));
+    if (getenv("WRITEBW_ORDER")) {
+        // the cfg3 generator's store order (fill_tiles), 2 passes
+        for (int pass = 0; pass < 2; pass++) {
+            printf("-- order pass %d\n", pass);
+#define TIL(AUX, CT, MODE, NAME)                                                            \
+    rep("tiles CT " #CT " " NAME " aux " #AUX, b3, timeit([&] {                               \
+            fill_tiles<AUX, CT, MODE><<<S3 * (2048 / CT), 256>>>(out, S3);                    \
+        }, 10));
+            TIL(0, 512, 0, "8 rows x 128 B") TIL(18, 512, 0, "8 rows x 128 B")
+            TIL(0, 512, 1, "row runs 1 KiB") TIL(18, 512, 1, "row runs 1 KiB")
+            TIL(0, 1024, 0, "8 rows x 128 B") TIL(18, 1024, 0, "8 rows x 128 B")
+            TIL(0, 1024, 1, "row runs 1 KiB") TIL(18, 1024, 1, "row runs 1 KiB")
+            TIL(0, 2048, 0, "8 rows x 128 B") TIL(18, 2048, 0, "8 rows x 128 B")
+            TIL(0, 2048, 1, "row runs 1 KiB") TIL(18, 2048, 1, "row runs 1 KiB")
+            // occupancy: the product's LDS footprint (77 KB: 2 blocks of 4
+            // waves per CU) or half of it, and 8-wave blocks
+            for (int lds : {77 * 1024, 38 * 1024, 19 * 1024}) {
+                CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fill_tiles<18, 512, 0, 4>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+                CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fill_tiles<18, 512, 0, 8>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+                char nm[96];
+                snprintf(nm, sizeof nm, "tiles CT 512 aux 18, 4 waves, LDS %d KB", lds >> 10);
+                rep(nm, b3, timeit([&] { fill_tiles<18, 512, 0, 4><<<S3 * 4, 256, lds>>>(out, S3); }, 10));
+                snprintf(nm, sizeof nm, "tiles CT 512 aux 18, 8 waves, LDS %d KB", lds >> 10);
+                rep(nm, b3, timeit([&] { fill_tiles<18, 512, 0, 8><<<S3 * 4, 512, lds>>>(out, S3); }, 10));
+            }
+        }
+        return 0;
+    }
     for (int pass = 0; pass < 2; pass++) {
         printf("-- pass %d\n", pass);
         LIN(0, "default", b3) LIN(2, "nt", b3) LIN(16, "sc1", b3) LIN(18, "nt|sc1", b3)
