@@ -53,7 +53,11 @@ int qi_gpu_device_count(void);
  *     multiple of 1024 columns and whose rows are 8-byte aligned inside
  *     31-bit buffer ranges (the encode only while the generator stays small:
  *     k * n_outputs <= 2^21, 2^18 systematic); the NTT engine otherwise;
- *   - k > 384: the NTT engine (column-batched NTT passes in LDS or HBM). */
+ *   - 384 < k <= 640, non-systematic, n - k > 64: the decode as above on
+ *     the matrix cores (k x k contexts, two K chunks); the encode, and every
+ *     other batch, on the NTT engine;
+ *   - k > 384 otherwise: the NTT engine (column-batched NTT passes in LDS or
+ *     HBM; the erasure decode when n - k <= 64). */
 qi_plan* qi_plan_create(int k, int m, int systematic);
 /* The same with flags: QI_PLAN_ENC_MATRIX / QI_PLAN_ENC_CODELETS force the
  * matrix-core or the register-codelet non-systematic encode for k <= 64
@@ -83,8 +87,9 @@ int qi_gpu_encode(qi_plan* plan, const uint16_t* d_data,
 /* Bytes of device workspace for n_stripes decode contexts of `words`
  * columns each -- enough for any width up to `words`.  A context is valid
  * only for the `words` it was built with (its format and per-stripe stride
- * follow the width: for 256 < k <= 384, matrix contexts at multiples of
- * 1024 columns, the NTT engine's otherwise). */
+ * follow the width: for 256 < k <= 384 (and the non-systematic 384 < k <=
+ * 640 codes with n - k > 64), matrix contexts at multiples of 1024 columns,
+ * the NTT engine's otherwise). */
 size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
                                long long words);
 
@@ -99,11 +104,11 @@ size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
  * reads the marks from them directly (slightly slower per tile than routed
  * tables).  Built on the device, asynchronously on `stream`, for every k:
  * matrix contexts (the interpolation matrix, up to ~780 KB per stripe at
- * k = 256) for k <= 256, and for 256 < k <= 384 at widths that are a
+ * k = 256) for k <= 256, and for 256 < k <= 384 (non-systematic: 640) at widths that are a
  * multiple of 1024 columns (then followed by the NTT engine's context, used
  * when the decode's rows are not addressable by the matrix cores); the NTT
  * decode's per-pattern constants (src/fec_context.h:232-274, whose decode
- * reads the OOR buckets directly) otherwise; for 256 < k <= 384 the NTT
+ * reads the OOR buckets directly) otherwise; for 256 < k <= 640 the NTT
  * engine's half is built by the first decode that needs it.  h_ids is
  * unused (kept for ABI stability; may be NULL). */
 int qi_gpu_decode_ctx(qi_plan* plan, const uint16_t* d_ids,
@@ -121,7 +126,7 @@ int qi_gpu_decode_ctx(qi_plan* plan, const uint16_t* d_ids,
  * The context is not const in effect: a decode whose rows the matrix cores
  * cannot address fills the context's lazily built sections (the dot2
  * kernel's packed rows for k <= 256, the NTT engine's half for 256 < k <=
- * 384) the first time, on `stream`, and records that in the context.  So a
+ * 640) the first time, on `stream`, and records that in the context.  So a
  * context may serve any number of decodes on one stream, but must not be
  * used by decodes on two streams at once. */
 int qi_gpu_decode(qi_plan* plan, const void* d_ctx, const uint16_t* d_ids,

@@ -4,6 +4,7 @@
 // and the OOR route tables of decode_prepare (src/fec_base.h:1361-1404).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 
 #include "gf65537.h"
@@ -163,7 +164,7 @@ __device__ __forceinline__ uint32_t grp_add(uint32_t v, int lpr)
         v += __shfl_xor(v, m, lpr);
     return v;
 }
-__device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLayout& L,
+__device__ __forceinline__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLayout& L,
                              int t, int32_t* block, int sub, int lpr, bool dot2)
 {
     // the lane's entries i = sub + m lpr (m < 16: k <= 256 at lpr = 16) in
@@ -248,28 +249,39 @@ __device__ void pack_row_grp(uint32_t* row, const uint32_t* cscale, const MatLay
 // the columns' 1 / A'(x_i), row-scaled when an entry breaks coef_ok (as
 // pack_row_grp: the row's scale search on its 32-lane group), summed into
 // kcorr / kmf, and written as the [a | 0], [0 | b], [b | a] operand tiles.
-// 4-entry groups per row of a context matrix, at most
-constexpr int kPackNj = kMatMaxKin / 4;
 // rows per chunk of the non-systematic k > 128 contexts (decode_ctx_kernel):
-// (the kernel's static LDS + kCtxChunk * kMatMaxKin * 4 bytes must fit
-// kCtxLdsCap; launch_decode_ctx checks)
+// (the kernel's static LDS + the largest chunk, ctx_chunk(k) rows x k
+// entries, must fit kCtxLdsCap; launch_decode_ctx checks)
 // 64 rows = 4 row blocks per packing pass at 16 lanes per row (32 rows at 32
 // lanes: twice the passes and barriers for the same work; contexts k256
-// 120 -> 114 us, k300 179 -> 161 us, k384 219 -> 206 us)
+// 120 -> 114 us, k300 179 -> 161 us, k384 219 -> 206 us); 32 rows above
+// k = 384 (a 64 x 640 chunk would not fit LDS)
 constexpr int kCtxChunk = 64;
+__host__ __device__ inline int ctx_chunk(int k)
+{
+    return k > kMatGenMaxKin ? 32 : kCtxChunk;
+}
 constexpr int kCtxLdsCap = 160 * 1024;
+// the packing stage's rows of (aw, bw) words (pitch 2 nj = 8 KS words, at
+// most 64 rows x 192 or 32 rows x 320), aliased with the A(x) product tree's
+// two level buffers (the tree is done before any packing)
+constexpr int kPackStg = 12288;
+constexpr int kTreeBuf = 2 * 512 + 4;
+static_assert(2 * kTreeBuf <= kPackStg, "tree buffers inside the packing stage");
 
 // One pass: NT / LPR rows from row block rb0 on (LPR lanes per row); row
 // t's canonical entries i0 .. i0 + 3 from ent(t, i0, e).  stg: a row per
 // pass row of the (aw, bw) words of each group (LDS).
 template <int NT, int LPR, class Ent>
-__device__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, const MatLayout& L,
-                                int32_t* mat, uint32_t (*stg)[2 * kPackNj])
+__device__ __forceinline__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, const MatLayout& L,
+                                int32_t* mat, uint32_t* stg_base)
 {
     constexpr int ROWS = NT / LPR;
-    constexpr int MM = (kMatMaxKin / 4 + LPR - 1) / LPR;
+    // 16 lanes per row: the 64-row chunks of k <= 384; 32: k <= 640
+    constexpr int MM = ((LPR <= 16 ? kMatGenMaxKin : kMatMaxKin) / 4 + LPR - 1) / LPR;
     static_assert(ROWS % 16 == 0, "whole row blocks per pass");
     const int k = L.kin, KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
+    auto stg = [&](int r, int c) -> uint32_t& { return stg_base[r * 2 * nj + c]; };
     const int tid = threadIdx.x, sub = tid % LPR, rl = tid / LPR;
     int32_t* mf = mat + L.mf();
     {
@@ -325,8 +337,8 @@ __device__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, c
                 }
                 const int jg = sub + m * LPR;
                 if (jg < nj) {
-                    stg[rl][2 * jg] = aw;
-                    stg[rl][2 * jg + 1] = bw;
+                    stg(rl, 2 * jg) = aw;
+                    stg(rl, 2 * jg + 1) = bw;
                 }
             }
             sum = grp_add(sum, LPR);
@@ -342,7 +354,7 @@ __device__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, c
             }
         } else {
             for (int jg = sub; jg < nj; jg += LPR)
-                stg[rl][2 * jg] = stg[rl][2 * jg + 1] = 0;
+                stg(rl, 2 * jg) = stg(rl, 2 * jg + 1) = 0;
         }
         __syncthreads();
         // the two row blocks' tile dwords, rows fastest (whole 128-byte tile
@@ -352,7 +364,7 @@ __device__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, c
         for (int it = tid; it < nrb * nj * 16; it += NT) {
             const int tl = it & 15, jj = it >> 4;
             const int jg = jj % nj, rbl = jj / nj, rb = rb0 + rbl;
-            const uint32_t aw = stg[16 * rbl + tl][2 * jg], bw = stg[16 * rbl + tl][2 * jg + 1];
+            const uint32_t aw = stg(16 * rbl + tl, 2 * jg), bw = stg(16 * rbl + tl, 2 * jg + 1);
 #pragma unroll
             for (int half = 0; half < 2; half++) {
                 const int K = half * KH + 4 * jg;
@@ -372,8 +384,8 @@ __device__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, c
 }
 
 template <int NT>
-__device__ void pack_tiles_direct(const uint32_t* Mt, int kp, const uint32_t* cinv,
-                                  const MatLayout& L, int32_t* mat, uint32_t (*stg)[2 * kPackNj])
+__device__ __forceinline__ void pack_tiles_direct(const uint32_t* Mt, int kp, const uint32_t* cinv,
+                                  const MatLayout& L, int32_t* mat, uint32_t* stg)
 {
     auto ent = [&](int t, int i0, uint32_t (&e)[4]) {
 #pragma unroll
@@ -486,7 +498,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // explicitly, so k = 64 u needs no extra slot.  Stored balanced.
     // (BIG: the product tree's levels, then the split Horner chains of the
     // A'(x_i))
-    __shared__ int32_t pt[2][2 * 512 + 4];
+    __shared__ __attribute__((aligned(16))) uint32_t big_lds[BIG ? kPackStg : 2 * kTreeBuf];
+    int32_t(*pt)[kTreeBuf] = reinterpret_cast<int32_t(*)[kTreeBuf]>(big_lds);
     if constexpr (BIG) {
         // k > 128: A(x) by a product tree instead of k dependent steps on one
         // wave (k = 256: 256 steps x 4 coefficient slots of DPP shifts and
@@ -576,7 +589,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         if (tid == 0)
             A[k] = 1;
     } else if (tid < 64) {  // wave 0 (wave-uniform)
-        constexpr int NS = kMatMaxKin / 64;
+        constexpr int NS = kMatGenMaxKin / 64;
         const int nslot = (k + 63) / 64;
         int32_t xv[NS], au[NS];
 #pragma unroll
@@ -718,7 +731,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     }
     __syncthreads();
     if constexpr (BIG) {
-        __shared__ uint32_t stg[kCtxChunk][2 * kPackNj];
+        uint32_t* stg = big_lds;  // the tree's buffers are dead now
         if (!dot2 && mode == 0) {
             // whole-tile widths, non-systematic: the rows in 64-row chunks
             // from the top, never in global memory.  Thread i runs Q_i's
@@ -728,19 +741,20 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             // entries per lane and group: scale, split, staged, stored
             // rows-fastest as whole tile lines).  No `plain` rows, no dot2
             // section (the kernels take single coefficients from the tiles).
-            uint32_t* ch = qi_ctx_lds;  // kCtxChunk x kpc
+            uint32_t* ch = qi_ctx_lds;  // CH x kpc
+            const int CH = ctx_chunk(k);
             const int kpc = (k + 3) & ~3;
             const int32_t xi = tid < k ? balanced(xs[tid]) : 0;
             const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
             // this block's chunks [c0, c1): the division runs down from the
             // top through the rows above them without keeping them
-            const int nch = (k + kCtxChunk - 1) / kCtxChunk;
+            const int nch = (k + CH - 1) / CH;
             const int c0 = (cb * nch + nb - 1) / nb, c1 = ((cb + 1) * nch + nb - 1) / nb;
             int32_t q = 1;  // coef_{k-1}(Q_i)
             if (tid < k)
-                q = div_steps(Ab, xi, q, k - 2, kCtxChunk * c1, [](int, int32_t) {});
+                q = div_steps(Ab, xi, q, k - 2, CH * c1, [](int, int32_t) {});
             for (int c = c1 - 1; c >= c0; c--) {
-                const int lo = kCtxChunk * c, hi = min(k, lo + kCtxChunk);
+                const int lo = CH * c, hi = min(k, lo + CH);
                 if (tid < k) {
                     auto keep = [&](int t, int32_t qt) { ch[(t - lo) * kpc + tid] = canon_lz(qt); };
                     if (hi == k)
@@ -756,7 +770,10 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                     e[3] = v.w;
                 };
                 // (ends with a barrier)
-                pack_tiles_pass<NT, NT / kCtxChunk>(lo >> 4, ent, cinv, L, mat, stg);
+                if (CH == kCtxChunk)
+                    pack_tiles_pass<NT, NT / kCtxChunk>(lo >> 4, ent, cinv, L, mat, stg);
+                else
+                    pack_tiles_pass<NT, NT / 32>(lo >> 4, ent, cinv, L, mat, stg);
             }
             return;
         }
@@ -1305,7 +1322,7 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
         // chunks of the matrix in the dynamic LDS; the systematic and dot2
         // forms keep the rows in global memory and reserve none)
         const size_t lds = mode == 0 && !dot2
-                               ? static_cast<size_t>(kCtxChunk) * ((k + 3) & ~3) * 4
+                               ? static_cast<size_t>(ctx_chunk(k)) * ((k + 3) & ~3) * 4
                                : 0;
         static std::atomic<uint64_t> attr_done{0};
         static std::atomic<int> cus_of[64];
@@ -1321,7 +1338,8 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
             if (bit)
                 cus_of[dev].store(std::max(1, cus), std::memory_order_relaxed);
             const void* fn = reinterpret_cast<const void*>(&decode_ctx_kernel<1024, true>);
-            constexpr size_t kDynMax = static_cast<size_t>(kCtxChunk) * kMatMaxKin * 4;
+            constexpr size_t kDynMax =
+                std::max(static_cast<size_t>(kCtxChunk) * kMatGenMaxKin, size_t{32} * kMatMaxKin) * 4;
             // the kernel's static LDS (the packing stage, A, x_i, ...) plus
             // the largest chunk must fit a CU (160 KiB): an added __shared__
             // would make every k > 256 context launch fail, so say so here
@@ -1339,7 +1357,7 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
         int nb = 1;
         if (mode == 0 && !dot2) {
             const int cus = bit ? cus_of[dev].load(std::memory_order_relaxed) : 256;
-            const int nch = (k + kCtxChunk - 1) / kCtxChunk;
+            const int nch = (k + ctx_chunk(k) - 1) / ctx_chunk(k);
             nb = std::max(1, std::min(nch, cus / S));
         }
         if (static_cast<long long>(S) * nb > 0x7fffffffLL)

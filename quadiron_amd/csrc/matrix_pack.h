@@ -32,21 +32,25 @@ namespace qi {
 // LDS-transposed streaming stores vs 1.62 ms dot2 (1.65 ms before the
 // transpose); the 48 x 16 systematic encode 3.60 vs 3.80 ms and the 64 x 64
 // decode 0.35 vs 0.62 ms.
-// the largest k the matrix kernels take (256 < k <= 384: whole 1024-column
-// tiles only, on the operand-stationary kernel; the NTT engine otherwise)
-constexpr int kMatMaxKin = 384;
+// the largest k the matrix kernels take (256 < k <= 640: whole 1024-column
+// tiles only, on the operand-stationary kernel; the NTT engine otherwise;
+// 384 < k <= 640: non-systematic decodes only, KS = 40 in two K chunks)
+constexpr int kMatMaxKin = 640;
+// the largest k of the matrix-core encodes and systematic codes (KS <= 24)
+constexpr int kMatGenMaxKin = 384;
 
 struct MatLayout {
     int R, kin, KP;
     // K-steps of 32 bytes over the [h' ; l'] planes; past 256 inputs only
     // the operand-stationary kernel takes the matrix (KS a multiple of 4,
-    // its double-buffered image <= 2 x 61 KB at KS = 24)
+    // its double-buffered image <= 2 x 61 KB at KS = 24; KS = 40 stages its
+    // image in two K chunks of 20 steps)
     QI_HD int KS() const
     {
         if (kin > kMatMaxKin)
             return 0;
         return kin <= 16 ? 1 : kin <= 32 ? 2 : kin <= 64 ? 4 : kin <= 128 ? 8
-               : kin <= 256 ? 16 : kin <= 320 ? 20 : 24;
+               : kin <= 256 ? 16 : kin <= 320 ? 20 : kin <= 384 ? 24 : 40;
     }
     QI_HD int RB() const { return KS() ? (R + 15) / 16 : 0; }
     QI_HD size_t packed() const { return 0; }
@@ -157,7 +161,7 @@ QI_HD uint32_t pack_row(const uint32_t* row, const MatLayout& L, int t,
 // `plain` section, or a copy of it in LDS).
 QI_HD int32_t pack_mf_dword(const MatLayout& L, const int32_t* rows, size_t d)
 {
-    const int KS = L.KS(), KH = 16 * KS;  // KS is 1, 2, 4, 8, 16, 20 or 24
+    const int KS = L.KS(), KH = 16 * KS;  // KS is 1, 2, 4, 8, 16, 20, 24 or 40
     const int tile = static_cast<int>(d >> 7);
     const int rem = static_cast<int>(d & 127), lane = rem >> 1, dw = rem & 1;
     const int ty = tile % 3, rk = tile / 3;

@@ -1659,7 +1659,7 @@ static bool eras_c2(const XfPlan& pni)
 
 bool eras_plan(const qi_plan* p)
 {
-    return p->ntt && !p->mbig && p->n <= kLdsMaxN && p->n - p->k <= kErasMax;
+    return p->ntt && !p->mbig && eras_shape(p->k, p->n);
 }
 
 ErasCtxLayout eras_layout(const qi_plan* p)
@@ -1904,6 +1904,11 @@ static int launch_ntt_ctx(const qi_plan* p, const NttCtxArgs& a, int S, hipStrea
     hipLaunchKernelGGL(ntt_ctx_kernel, dim3(S, (items + kNttBlock - 1) / kNttBlock),
                        dim3(kNttBlock), lds, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+bool eras_shape(int k, int n)
+{
+    return n <= kLdsMaxN && n - k <= kErasMax;
 }
 
 long long ntt_ctx_words(const qi_plan* p)

@@ -38,6 +38,8 @@ static bool enc_matrix(int K, int flags)
 // memory and seconds of host time for the systematic Lagrange rows)
 static bool big_generator_ok(int k, int n_outputs, int sys)
 {
+    if (k > kMatGenMaxKin)
+        return false;  // 384 < k <= 640: the matrix cores decode only
     const long long e = static_cast<long long>(k) * n_outputs;
     return e <= (sys ? (1LL << 18) : (1LL << 21));
 }
@@ -187,7 +189,13 @@ qi_plan* qi_plan_create_ex(int k, int m, int systematic, int flags)
         // (qi_gpu.cpp use_matrix: words a multiple of 1024), with the
         // generator below and per-stripe k x k contexts
         p->ntt = 1;
-        p->mbig = k <= kMatMaxKin ? 1 : 0;
+        // 384 < k <= 640: the non-systematic decodes on the matrix cores
+        // (KS = 40, two K chunks), unless the code misses few symbols (the
+        // erasure decode's O(e^2 + n log n) per column beats O(k^2))
+        p->mbig = k <= kMatGenMaxKin ||
+                          (k <= kMatMaxKin && !p->sys && !eras_shape(k, p->n))
+                      ? 1
+                      : 0;
         ok = ntt_plan_init(p) == 0;
     }
     if (ok && (!p->ntt || p->mbig)) {

@@ -86,7 +86,9 @@ struct qi_plan {
     // encode's constant decode context
     int ntt = 0, len2k = 0, nmax = 0;
     // 256 < k <= 384: batches whose columns tile exactly (words a multiple
-    // of 1024) run the matrix cores instead (d_gen, k x k contexts)
+    // of 1024) run the matrix cores instead (d_gen, k x k contexts); also
+    // 384 < k <= 640, non-systematic, n - k > 64: the decodes only (no
+    // generator; the encode stays on the NTT engine)
     int mbig = 0;
     int32_t* d_tw[2] = {nullptr, nullptr};
     int32_t* d_ldstw = nullptr;  // per-pass twiddle tables of the LDS engine
@@ -98,6 +100,8 @@ struct qi_plan {
 namespace qi {
 // ---- general-k path (ntt.hip) ----
 int ntt_plan_init(qi_plan* p);
+// the erasure decode's shape (n <= 2048, n - k <= 64; ntt.hip)
+bool eras_shape(int k, int n);
 // the NTT engine's kernels for an encode or a decode (a decode's list starts
 // with its context builder): ntt_eras_kernel<TWG> (few erasures), ntt_lds_kernel<TWG>
 // (max(n, len_2k) <= 2048) or the multi-pass engine

@@ -339,6 +339,10 @@ def main():
     gen_blocks(ref, ora, "blk_k500_m12_sys", 500, 12, 1, 128, 512, 46, 2, 8, out)
     gen_blocks(ref, ora, "blk_k2000_m48", 2000, 48, 0, 32, 128 + 2, 47, 2, 8, out)
 
+    # 384 < k <= 640 at a whole 1024-word tile: the decode on the matrix
+    # cores at KS = 40 in two K chunks (round 6)
+    gen_blocks(ref, ora, "blk_k400_m100_w1024", 400, 100, 0, 256, 2048, 55, 1, 10, out)
+
     def gen_scn(*a):
         if not only or a[2] in only:
             _gen_cabi_scn(*a)

@@ -159,7 +159,7 @@ static void test_matrix(std::mt19937_64& g)
 
 static void test_matrix_mfma(std::mt19937_64& g)
 {
-    for (int kin : {1, 3, 16, 17, 33, 64, 65, 100, 128, 129, 200, 256}) {
+    for (int kin : {1, 3, 16, 17, 33, 64, 65, 100, 128, 129, 200, 256, 300, 384, 385, 600, 640}) {
         for (int R : {kin, 48}) {
             int KP = 2;
             while (KP < (kin + 1) / 2)
@@ -229,7 +229,8 @@ static void test_matrix_mfma(std::mt19937_64& g)
                     }
                     for (long long d : D)
                         CHECK(d >= -2147483648LL && d <= 2147483647LL, "mfma acc overflow");
-                    // KS = 16 (k > 128): the device folds D2 before the shift
+                    // KS >= 16 (k > 128): the device folds D2 before the shift (KS = 40:
+                    // the two K chunks accumulate into the same D0, D1, D2)
                     const long long d2 = KS >= 16 ? fold(static_cast<int32_t>(D[2])) : D[2];
                     const long long v = d2 * 256 + D[1] - D[0];
                     CHECK(v >= -2147483648LL && v <= 2147483647LL, "mfma epilogue overflow");

@@ -353,8 +353,15 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True,
     (257, 255, 0, 1, 2048),
     (320, 100, 1, 2, 1024),   # systematic: generator + mode-1 contexts
     (321, 63, 0, 2, 1024),    # KS = 24
-    (384, 128, 0, 1, 2048),   # largest matrix-path k
+    (384, 128, 0, 1, 2048),   # largest generator / systematic matrix-path k
     (384, 100, 1, 1, 1024),
+    # 384 < k <= 640, non-systematic, n - k > 64, whole 1024-column tiles:
+    # the decode on the matrix cores at KS = 40 in two K chunks (round 6;
+    # the encode stays on the NTT engine)
+    (385, 127, 0, 2, 1024),   # smallest KS = 40 code
+    (500, 524, 0, 1, 2048),
+    (600, 1400, 0, 1, 1024),  # the k600 bench code
+    (640, 384, 0, 1, 1024),   # largest matrix-path k
     # k > 256: the NTT-structured general path (ntt.hip)
     (257, 255, 0, 1, 300),    # smallest NTT-path code
     (300, 100, 1, 1, 300),    # systematic: interpolation + NTT_n encode

@@ -46,7 +46,10 @@ def test_reported_kernels_exist(cfg, sys_):
     dec = kernels.split("; ")[1]
     assert "ctx_" in dec.split(" + ")[0] or dec.startswith("decode=ntt_ctx_kernel")
 
-    # 256 < k <= 384 at whole-tile widths: the NTT engine's context is built
-    # only by a decode the matrix cores cannot take
-    if cfg in ("k300", "k384"):
+    # 256 < k <= 640 at whole-tile widths: the NTT engine's context is built
+    # only by a decode the matrix cores cannot take; the
+    # k600 decode runs the matrix cores at KS = 40 (round 6)
+    if cfg in ("k300", "k384", "k600"):
         assert "ntt_ctx_kernel" not in dec, kernels
+    if cfg == "k600":
+        assert "matrix_os_kernel<40, 8, 1, false>" in dec, kernels
