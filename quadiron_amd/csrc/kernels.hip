@@ -687,8 +687,10 @@ constexpr int kRedoSpan = 64;
 
 __global__ __launch_bounds__(kBlock) void matrix_redo_kernel(MatArgs a, int n_stripes)
 {
-    __shared__ uint16_t xs[kMatMaxKin * kRedoCols];  // [input i][column]
-    __shared__ uint32_t mk[kMatMaxKin * (kRedoCols / 32)];
+    // (the dot2 tails' slow tiles: k <= 256; the operand-stationary kernel
+    // redoes its own in its dynamic LDS)
+    __shared__ uint16_t xs[kMatGenMaxKin * kRedoCols];  // [input i][column]
+    __shared__ uint32_t mk[kMatGenMaxKin * (kRedoCols / 32)];
     __shared__ uint32_t colmk[kRedoCols / 32];
     const int tid = threadIdx.x, c = tid & 63, wv = tid >> 6;
     // this block's stripes with a non-empty list (wave 0, one lane each;
@@ -1861,6 +1863,17 @@ __device__ __forceinline__ int32_t pick_v4(const qi_v4i (&v)[NP], int idx)
     return r;
 }
 
+// K chunks of the operand-stationary kernel: KS = 40 (384 < k <= 640) stages
+// its image in two chunks of 20 K-steps (the received rows [0, 320) and
+// [320, 640)), double-buffered over (tile, chunk) items, the accumulators
+// held across the chunks of a tile: a whole KS = 40 image (2 x 640 rows of
+// 80 bytes, 102 KB) could not be double-buffered in LDS
+template <int KS>
+struct OsK {
+    static constexpr int NCH = KS > 24 ? 2 : 1;  // K chunks per tile
+    static constexpr int KC = KS / NCH;          // K-steps per chunk
+};
+
 template <int KS, int WR>
 struct OsTile {
     static constexpr int kWaves = 8;
@@ -1886,9 +1899,11 @@ struct OsTile {
 template <int KS, int WR, int RPW, bool TWO>
 __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C, int TS)
 {
-    using O = OsTile<KS, WR>;
+    constexpr int NCH = OsK<KS>::NCH, KC = OsK<KS>::KC;
+    using O = OsTile<KC, WR>;  // one chunk's image (the whole K when NCH = 1)
     constexpr int KH = O::kRows, RSB = O::kPitch, RPT = O::kRpt, NCOL = O::kCols;
-    static_assert(KS % 4 == 0, "x64 pairs with zero halves");
+    static_assert(KS % 4 == 0 && KC % 4 == 0, "x64 pairs with zero halves");
+    static_assert(NCH == 1 || (RPW == 1 && !TWO), "K chunks: one row block per wave, one region");
     extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
     const MatLayout L = a.L;
     const RowSrc src = a.src;
@@ -1987,21 +2002,24 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     const Region<true> go(dst.base + s * dst.ss, ext.eo);
     const int rowgrp = tid / O::kTpr, cl = (tid % O::kTpr) * 4;
     constexpr uint32_t kOob = 0x80000000u;  // past any extent (< 2^31)
-    uint32_t off0[RPT], off1[TWO ? RPT : 1];
+    // (chunk c stages the received rows KH c .. KH c + KH - 1)
+    uint32_t off0[NCH][RPT], off1[TWO ? RPT : 1];
 #pragma unroll
-    for (int r = 0; r < RPT; r++) {
-        const int i = O::kRpp * r + rowgrp;
-        const int ii = i < kin ? i : kin - 1;
-        const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
-        const uint32_t lane = static_cast<uint32_t>(cl * 2);
-        if constexpr (TWO) {
-            const bool lo = id < src.split;
-            off0[r] = lo ? static_cast<uint32_t>(id * src.rs0 * 2) + lane : kOob;
-            off1[r] = lo ? kOob : static_cast<uint32_t>((id - src.split) * src.rs1 * 2) + lane;
-        } else {
-            off0[r] = static_cast<uint32_t>(id * src.rs0 * 2) + lane;
+    for (int c = 0; c < NCH; c++)
+#pragma unroll
+        for (int r = 0; r < RPT; r++) {
+            const int i = KH * c + O::kRpp * r + rowgrp;
+            const int ii = i < kin ? i : kin - 1;
+            const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
+            const uint32_t lane = static_cast<uint32_t>(cl * 2);
+            if constexpr (TWO) {
+                const bool lo = id < src.split;
+                off0[c][r] = lo ? static_cast<uint32_t>(id * src.rs0 * 2) + lane : kOob;
+                off1[r] = lo ? kOob : static_cast<uint32_t>((id - src.split) * src.rs1 * 2) + lane;
+            } else {
+                off0[c][r] = static_cast<uint32_t>(id * src.rs0 * 2) + lane;
+            }
         }
-    }
     // DEEP (KS = 4, the short decodes): ND tiles of rows in flight per
     // block (a ring of ND register sets, 8 VGPRs each) -- with one, a CU
     // kept ~32 KB of loads in flight and the cfg3 decode was bound by the
@@ -2013,13 +2031,14 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     // rows of `tile` into wr; an invalid tile (past the block's range) loads
     // from past the buffer's extent (no memory access, zeros), so the number
     // of loads in flight is the same on every path
-    auto issue_rows_to = [&](int tile, bool valid, auto& wr) {
+    auto issue_rows_to = [&](int tile, bool valid, auto& wr, auto cc) {
+        constexpr int c = decltype(cc)::value;  // K chunk
         const int so = valid ? tile * NCOL * 2 : 0;  // byte offset of the tile's first column
         const uint32_t oob = valid ? 0u : kOob;
 #pragma unroll
         for (int r = 0; r < RPT; r++) {
             const auto v = __builtin_amdgcn_raw_buffer_load_b64(
-                g0.r, static_cast<int>(off0[r] | oob), so, kAuxLdOs);
+                g0.r, static_cast<int>(off0[c][r] | oob), so, kAuxLdOs);
             wr[r][0] = v[0];
             wr[r][1] = v[1];
             if constexpr (TWO) {
@@ -2030,7 +2049,8 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             }
         }
     };
-    auto issue_rows = [&](int tile) { issue_rows_to(tile, true, w); };
+    using C0 = std::integral_constant<int, 0>;
+    auto issue_rows = [&](int tile, auto cc) { issue_rows_to(tile, true, w, cc); };
     const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) + 4 * ((cl % 64) / 16);
     auto write_rows_from = [&](uint8_t* img, const auto& w) {
 #pragma unroll
@@ -2106,47 +2126,60 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
 
     // row block j of this wave over its super tile (columns col0 ..
     // col0 + 63) from image img
-    auto compute = [&](const uint8_t* img, long long col0, int n_lm, const int* mi,
-                       const uint32_t* mc, auto jc, auto&& before_stores) {
+    // row block j's accumulators: D0 = 0, D1 = kmf (the byte offsets'
+    // correction), D2 = 0
+    auto init_acc = [&](qi_v4i (&acc)[4][3], auto jc) {
         constexpr int j = decltype(jc)::value;
-        auto* lds = (__attribute__((address_space(3))) const uint8_t*)img;
-        const int t = 16 * rbj[j] + tl;
-        const bool trow = act[j] && t < L.R;
-        qi_v4i acc[4][3];
 #pragma unroll
         for (int T = 0; T < 4; T++) {
             acc[T][0] = qi_v4i{0, 0, 0, 0};
             acc[T][1] = qi_v4i{kt[j], kt[j], kt[j], kt[j]};
             acc[T][2] = qi_v4i{0, 0, 0, 0};
-            // the h' half of K (pairs 0 .. KS/4-1: [a|0] and [b|a]), then the
-            // l' half ([0|b] and [b|a]): KS / 4 A pairs live at a time
+        }
+    };
+    // K chunk cc of row block j over this wave's super tile of image img,
+    // accumulated into acc: the chunk's h' half of K (its pairs: [a|0] and
+    // [b|a]), then its l' half ([0|b] and [b|a]), KC / 4 A pairs live at a
+    // time; operand pair c KC / 4 + i of the row block's registers
+    auto mma = [&](const uint8_t* img, qi_v4i (&acc)[4][3], auto jc, auto cc) {
+        constexpr int j = decltype(jc)::value, c = decltype(cc)::value;
+        auto* lds = (__attribute__((address_space(3))) const uint8_t*)img;
+#pragma unroll
+        for (int T = 0; T < 4; T++) {
 #pragma unroll
             for (int hf = 0; hf < 2; hf++) {
-                qi_v4i av[KS / 4];
+                qi_v4i av[KC / 4];
 #pragma unroll
-                for (int i = 0; i < KS / 4; i++) {
+                for (int i = 0; i < KC / 4; i++) {
                     auto rd = [&](int ks) {
                         auto* pa = (__attribute__((address_space(3))) qi_v2i*)(
                             lds + abase + 32 * ks * RSB + T * 16);
                         return __builtin_amdgcn_ds_read_tr8_b64_v2i32(pa);
                     };
-                    const int pi = hf * (KS / 4) + i;
+                    const int pi = hf * (KC / 4) + i;
                     const qi_v2i x0 = rd(2 * pi), x1 = rd(2 * pi + 1);
                     av[i] = qi_v4i{x0.x, x0.y, x1.x, x1.y};
                 }
 #pragma unroll
-                for (int i = 0; i < KS / 4; i++) {
+                for (int i = 0; i < KC / 4; i++) {
+                    constexpr int o = c * (KC / 4);
                     if (hf == 0)
-                        acc[T][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b0[j][i],
+                        acc[T][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b0[j][o + i],
                                                                           acc[T][0], 0, 0, 0);
                     else
-                        acc[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b1[j][i],
+                        acc[T][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[i], b1[j][o + i],
                                                                           acc[T][1], 0, 0, 0);
                     acc[T][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                        av[i], hf == 0 ? b1[j][i] : b0[j][i], acc[T][2], 0, 0, 0);
+                        av[i], hf == 0 ? b1[j][o + i] : b0[j][o + i], acc[T][2], 0, 0, 0);
                 }
             }
         }
+    };
+    auto epilogue = [&](const qi_v4i (&acc)[4][3], long long col0, int n_lm, const int* mi,
+                        const uint32_t* mc, auto jc, auto&& before_stores) {
+        constexpr int j = decltype(jc)::value;
+        const int t = 16 * rbj[j] + tl;
+        const bool trow = act[j] && t < L.R;
         // epilogue: lane (g, t) holds row t, columns cb .. cb + 15
         const long long cb = col0 + 16 * g;
         int32_t y[16];
@@ -2234,6 +2267,14 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     };
+    // the whole K in one image (NCH = 1)
+    auto compute = [&](const uint8_t* img, long long col0, int n_lm, const int* mi,
+                       const uint32_t* mc, auto jc, auto&& before_stores) {
+        qi_v4i acc[4][3];
+        init_acc(acc, jc);
+        mma(img, acc, jc, C0{});
+        epilogue(acc, col0, n_lm, mi, mc, jc, before_stores);
+    };
 
     auto idle_stores = [&]() {
 #pragma unroll
@@ -2250,7 +2291,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         // tiles t0 .. t0 + ND - 1 in flight, the first one into image 0
 #pragma unroll
         for (int d = 0; d < ND; d++)
-            issue_rows_to(t0 + d, t0 + d < t1, wring[d]);
+            issue_rows_to(t0 + d, t0 + d < t1, wring[d], C0{});
         write_rows_from(img(0), wring[0]);
         int nl[2];
         nl[0] = stage_marks(t0, 0);
@@ -2262,7 +2303,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             constexpr int J = decltype(jc)::value;
             const int b = (tile - t0) & 1;
             const bool more = tile + 1 < t1;  // block-uniform
-            issue_rows_to(tile + ND, tile + ND < t1, wring[J]);
+            issue_rows_to(tile + ND, tile + ND < t1, wring[J], C0{});
             const long long col0 = static_cast<long long>(tile) * NCOL + 64 * st;
             auto none = [] {};
             [&]<int... R>(std::integer_sequence<int, R...>) {
@@ -2295,18 +2336,63 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         finish();
         return;
     }
-    issue_rows(t0);
+    issue_rows(t0, C0{});
     write_rows(img(0));
     int nl[2];
     nl[0] = stage_marks(t0, 0);
     nl[1] = 0;
     __syncthreads();
+    if constexpr (NCH > 1) {
+        // (tile, chunk) items, double-buffered: item q's rows in image q & 1
+        // while item q + 1's are in flight; a tile's accumulators live over
+        // its chunks, its epilogue (marks, stores) after the last one
+        static_assert(NCH == 2, "two K chunks");
+        constexpr bool rows_first = true;
+        int ib = 0;
+#pragma unroll 1
+        for (int tile = t0; tile < t1; tile++) {
+            const int mb = (tile - t0) & 1;
+            const bool more = tile + 1 < t1;  // block-uniform
+            const long long col0 = static_cast<long long>(tile) * NCOL + 64 * st;
+            qi_v4i acc[4][3];
+            using J0 = std::integral_constant<int, 0>;
+            // chunk 0; chunk 1's rows in flight, staged right after
+            issue_rows(tile, std::integral_constant<int, 1>{});
+            init_acc(acc, J0{});
+            if (act[0])
+                mma(img(ib), acc, J0{}, C0{});
+            write_rows(img(ib ^ 1));
+            __syncthreads();
+            ib ^= 1;
+            // chunk 1, then the epilogue; the next tile's chunk 0 in flight
+            if (more)
+                issue_rows(tile + 1, C0{});
+            if (act[0])
+                mma(img(ib), acc, J0{}, std::integral_constant<int, 1>{});
+            auto stage_next = [&]() {
+                if (rows_first && more)
+                    write_rows(img(ib ^ 1));
+            };
+            if (act[0])
+                epilogue(acc, col0, nl[mb], s_i(mb), s_col(mb), J0{}, stage_next);
+            else {
+                stage_next();
+                idle_stores();
+            }
+            if (more)
+                nl[mb ^ 1] = stage_marks(tile + 1, mb ^ 1);
+            __syncthreads();
+            ib ^= 1;
+        }
+        finish();
+        return;
+    }
 #pragma unroll 1
     for (int tile = t0; tile < t1; tile++) {
         const int b = (tile - t0) & 1;
         const bool more = tile + 1 < t1;  // block-uniform
         if (more)
-            issue_rows(tile + 1);
+            issue_rows(tile + 1, C0{});
         const long long col0 = static_cast<long long>(tile) * NCOL + 64 * st;
         // an idle wave (row block past RB) issues the same two stores, past
         // the buffer's extent (dropped): with the store count equal on both
@@ -2461,8 +2547,10 @@ int matrix_kp(int kin)
         return 64;
     if (pairs <= 128)
         return 128;
-    if (2 * pairs <= kMatMaxKin + 1)
+    if (2 * pairs <= kMatGenMaxKin + 1)
         return 256;  // 256 < k <= 384: matrix cores only (no dot2 tails)
+    if (2 * pairs <= kMatMaxKin + 1)
+        return 320;  // 384 < k <= 640: (the context layout's unused section)
     return -1;  // larger k runs the NTT path (ntt.hip)
 }
 
@@ -2570,7 +2658,9 @@ constexpr long long kOsMaxTiles = 4096;  // tiles per block (slow-tile bitmask)
 template <int KS, int WR, int RPW>
 static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 {
-    using O = OsTile<KS, WR>;
+    using O = OsTile<OsK<KS>::KC, WR>;
+    // the systematic decodes' two source regions: KS <= 24 only (os_geom)
+    constexpr bool kTwo = RPW == 1 && OsK<KS>::NCH == 1;
     const long long TS = wfull / O::kCols;
     if (TS <= 0 || TS > 0x7fffffffLL)
         return -1;
@@ -2587,11 +2677,12 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
     const uint64_t bit = dev < 64 ? 1ull << dev : 0;
     if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
         // (two source regions only at RPW = 1, os_geom)
+        const void* two_fn = nullptr;
+        if constexpr (kTwo)
+            two_fn = reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, 1, true>);
         if (lds > 65536 &&
-            ((RPW == 1 && hipFuncSetAttribute(
-                              reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, 1, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds)) != hipSuccess) ||
+            ((two_fn && hipFuncSetAttribute(two_fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            static_cast<int>(lds)) != hipSuccess) ||
              hipFuncSetAttribute(
                  reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, false>),
                  hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2647,7 +2738,7 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
         return -1;
     a.tiles = static_cast<int>(TS);
     if (a.src.base1) {
-        if constexpr (RPW != 1)
+        if constexpr (!kTwo)
             return -1;  // not chosen by os_geom
         else
             hipLaunchKernelGGL((matrix_os_kernel<KS, WR, 1, true>),
@@ -2679,6 +2770,10 @@ inline OsGeom os_geom(int KS, int RB, bool two)
     // gpurun_out/ab_r5k, ab_r5l)
     if ((KS == 16 || KS == 20 || KS == 24) && RB > 8 && !two)
         return {8, 2};
+    // KS = 40 (384 < k <= 640, K chunks): non-systematic decodes only, one
+    // row block per wave (80 operand VGPRs)
+    if (KS > 24)
+        return two ? OsGeom{0, 0} : OsGeom{8, 1};
     if (KS >= 8)
         return {8, 1};
     // KS = 4: the short decode matrices (2 super tiles per 128-column tile)
@@ -2708,6 +2803,10 @@ static int mfma_dispatch(const MatArgs& a, long long wfull, int S, hipStream_t s
             return os_launch<KS, 8, 2>(a, wfull, S, st);
         if (og.wr)
             return os_launch<KS, 8, 1>(a, wfull, S, st);
+    } else if constexpr (KS == 40) {
+        if (os_geom(KS, a.L.RB(), a.src.base1 != nullptr).wr)
+            return os_launch<KS, 8, 1>(a, wfull, S, st);
+        return -1;
     }
     constexpr int NSTS = KS == 1 ? 16 : 8;
     const int RB = a.L.RB();
@@ -2791,8 +2890,10 @@ static int launch_matrix_kernels(MatArgs a, int S, hipStream_t st, bool* dot2)
             rc = mfma_dispatch<16>(a, wfull, S, st);
         else if (L.KS() == 20)
             rc = mfma_dispatch<20>(a, wfull, S, st);
-        else
+        else if (L.KS() == 24)
             rc = mfma_dispatch<24>(a, wfull, S, st);
+        else
+            rc = mfma_dispatch<40>(a, wfull, S, st);
         if (rc || wfull == words)
             return rc;
         a.ext.c0 = wfull;
