@@ -1915,14 +1915,27 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
     const int g = l >> 4, q = (l & 15) >> 1, p = l & 1, tl = l & 15;
 
-    // block -> (stripe, row-block group, column range); the G groups of one
-    // (stripe, range) on the same XCD when the units tile the 8 XCDs
+    // block -> (stripe, row-block group, column range); every block of one
+    // stripe on the same XCD (block b runs on XCD b % 8), consecutive in its
+    // dispatch order, when the stripes tile the 8 XCDs: the stripe's context
+    // tiles (256 KB per stripe at k = 256, 4 KiB packets: a quarter of its
+    // data bytes) and the input tiles its G groups share are read from HBM
+    // once and hit that XCD's L2 after (round 6: the C column ranges had
+    // landed on different XCDs, k256 decode reads 1.23x algorithmic);
+    // otherwise the G groups of one (stripe, range) on one XCD
     int s, gq, cr;
     {
         const int L0 = blockIdx.x;
         int unit;
         const int S = static_cast<int>(gridDim.x) / (G * C);
-        if (((S * C) & 7) == 0) {
+        if ((S & 7) == 0) {
+            const int x = L0 & 7, j = L0 >> 3, per = G * C;
+            const int sg = j / per, rem = j - sg * per;
+            s = sg * 8 + x;
+            cr = rem / G;
+            gq = rem - cr * G;
+            unit = s * C + cr;
+        } else if (((S * C) & 7) == 0) {
             const int x = L0 & 7, j = L0 >> 3;
             gq = j % G;
             unit = (j / G) * 8 + x;

@@ -786,6 +786,9 @@ def test_dense_tile_over_scratch_decodes(k, m):
     (256, 768, 5, [(64, 832)], 2048),
     # 256 < k <= 384, whole tiles: the operand-stationary kernel at KS = 20
     (300, 100, 5, [(0, 768)], 1024),
+    # 384 < k <= 640, whole tiles: KS = 40 in two K chunks (the redo's
+    # scratch for 400 inputs in the kernel's LDS)
+    (400, 100, 5, [(0, 768)], 1024),
     # k > 256, ragged width: the NTT engine walks the buckets itself (no
     # tile list)
     (300, 100, 5, [(0, 768)], 1000),
@@ -838,13 +841,13 @@ def test_dense_tiles_spread_decode(k, m, per_col, ranges, P):
     assert torch.equal(dec, dd)
 
 
-@pytest.mark.parametrize("k,m", [(16, 48), (100, 28), (200, 56), (300, 100)])
+@pytest.mark.parametrize("k,m", [(16, 48), (100, 28), (200, 56), (300, 100), (400, 100)])
 def test_decode_bucket_overflow_raises(k, m):
     """A decode reading an OOR bucket whose count exceeds its capacity lost
     marks: it must raise the plan's sticky error, not return wrong data
     silently (the reference returns -1 on header overflow,
     src/property.h:106-108).  k = 16, 100, 200: matrix cores at KS = 1, 8,
-    16; k = 300: the NTT engine."""
+    16; k = 300, 400: the operand-stationary kernel at KS = 20 / 40."""
     torch = _torch()
     plan, dd, out, P = _dense_tile_setup(k, m, 200, seed=5)
     cap = 2
