@@ -524,6 +524,19 @@ def test_cfg3_full_batch_vs_oracle():
                      windows=[(0, 128), (1024 - 64, 1024 + 64), (P - 128, P)])
 
 
+def test_cfg2_full_batch_vs_oracle():
+    """BASELINE configs[1] at its full bench size: 4096 stripes of k=16,
+    n=64, 64 KiB packets (4 GiB of data, 16 GiB coded), each decoded from its
+    own random 16-subset (the bench checks only the round trip):
+    every stripe round-trips through both decode layouts, and stripes 0, 128,
+    256, ..., 4095 match the oracle by column windows at the start, the
+    middle and the end of the packet (outputs, OOR lists, decodes)."""
+    P = 32768
+    _batch_roundtrip(16, 48, 0, 4096, P, seed=8, n_craft=8, check_oracle=False,
+                     oracle_stripes=_spread(4096, 128),
+                     windows=[(0, 128), (P // 2 - 64, P // 2 + 64), (P - 128, P)])
+
+
 @pytest.mark.parametrize("k,m,S,P", [
     (16, 48, 4096, 256),    # ~0.1 % of the stripes need a row scale
     (64, 960, 96, 1024),    # ~27 %
