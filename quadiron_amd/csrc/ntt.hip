@@ -529,7 +529,7 @@ struct NttLdsArgs {
     // the e x e solve in the context, n^-1 (balanced)
     int eras_e, eras_eid, eras_b;
     int32_t inv_n;
-    const int32_t* rinv;  // w_R^-x, x < R = 2^pni.lgr[0] (d_ldstw tail)
+    const int32_t* rinv;  // w_32^-x, x < 32 (d_ldstw tail): w_R^-x for every radix R
 };
 
 // One pass over the image: tasks (group start b, offset j < s) of the R
@@ -927,7 +927,8 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_lds_kernel(NttLdsArgs a)
 // then the last pass (q = 0: tasks j < s, positions j + u s) evaluates just
 // the outputs u >= ceil((k - j) / s) of its R-point inverse DFT directly
 // (y_u = sum_q v'_q w_R^-qu with the twiddled inputs v'; a handful per task)
-// instead of the whole codelet.  rinv: w_R^-x, x < R, balanced (R = 2^lgr[0]).
+// instead of the whole codelet.  rinv: w_32^-x, x < 32, balanced (w_R^-x =
+// w_32^(-x 32 / R) for the pass's radix R = 2^lgr[0]).
 // With syn (e x T, row t - k) the outputs go there and the image keeps the
 // state after the other passes (the two-pass decode completes the transform
 // from it); otherwise into the image rows t.
@@ -983,7 +984,7 @@ __device__ void lds_intt_top(int32_t* buf, const int32_t* tw, const XfPlan& P, i
 #pragma unroll
             for (int q = 1; q < 32; q++)
                 if (q < R)
-                    acc += mul_rt(v[q], rinv[(q * u) & (R - 1)]);
+                    acc += mul_rt(v[q], rinv[((q * u) << (5 - lgR)) & 31]);
             // output t = j + u s >= k: into syn (row t - k) when given,
             // leaving the image as the passes before the last left it
             if (syn)
@@ -1145,7 +1146,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
     int32_t* s_eid = s_pos + (C2 ? (e << lgT) : n);
     int32_t* s_B = s_eid + e;
     int32_t* s_cE = s_B + e * e;
-    int32_t* s_rinv = s_cE + (e << lgT);  // w_R^-x of INTT_n's last pass
+    int32_t* s_rinv = s_cE + (e << lgT);  // w_32^-x (INTT_n's passes' inverse roots)
     // C2: the syndromes y'_[k, n) (e x T <= n words, eras_launch) in the
     // position map's place (a non-systematic decode reads it no more)
     int32_t* s_syn = C2 ? s_pos : nullptr;
@@ -1170,7 +1171,7 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
         s_eid[j] = ctx[a.eras_eid + j];
     for (int i = tid; i < e * e; i += kLdsThreads)
         s_B[i] = ctx[a.eras_b + i];
-    if (tid < (1 << a.pni.lgr[0]))
+    if (tid < 32)
         s_rinv[tid] = a.rinv[tid];
     __syncthreads();
     const RowSrc& src = a.src;
@@ -1302,8 +1303,8 @@ __global__ __launch_bounds__(kLdsThreads) void ntt_eras_kernel(NttLdsArgs a)
                 for (int j = 0; j < e; j++) {
                     const int t = s_eid[j], q0 = t >> lg0;
                     int32_t* d = buf + (prow(((t & m0) << lg1) + u) << lgT) + c;
-                    // w_R1^-x = w_R0^(-x R0 / R1)
-                    const int32_t w = s_rinv[((q0 * u) << (lg0 - lg1)) & m0];
+                    // w_R1^-x = w_32^(-x 32 / R1)
+                    const int32_t w = s_rinv[((q0 * u) << (5 - lg1)) & 31];
                     *d = fold(fold(*d + mul_rt(s_cE[(j << lgT) + c], w)));
                 }
             }
@@ -1515,6 +1516,11 @@ NttCtxLayout ctx_layout_of(const qi_plan* p)
 // passes)
 XfPlan xf_plan(int N)
 {
+    // radices <= 32 as even as possible (2048: 16, 16, 8).  Round 6 tried the
+    // radix-32 unit pass the image's row padding keeps conflict-free (2048:
+    // 8, 8, 32; the k600 encode had 58 % of its LDS cycles in bank
+    // conflicts): 2.06-2.09 -> 2.17-2.26 ms, the radix-8 passes cost more
+    // than the conflicts (profiles/r6_ab_notes.txt), so the plan stays
     XfPlan P{};
     P.N = N;
     const int bits = ilog2i(N);
@@ -1580,16 +1586,16 @@ int lds_tables(const qi_plan* p, XfPlan* pl, std::vector<int32_t>* tab, int* twi
             off += (L + 3) & ~3;
         }
     }
-    // the inverse R-th roots of INTT_n's last DIT pass (R = its pass-0
-    // radix) for the erasure decode's pruned last pass (lds_intt_top)
+    // w_32^-x, x < 32: the inverse R-th roots of INTT_n's DIT passes for
+    // every radix R | 32 (w_R^-x = w_32^(-x 32 / R)), for the erasure
+    // decode's pruned last pass (lds_intt_top) and its two-pass completion
     if (rinv_off)
         *rinv_off = off;
     if (tab) {
-        const int R = 1 << pl[kTwPni].lgr[0];
         tab->resize(off + 32);
-        const uint32_t wi = invmod_c(root_of_unity(static_cast<uint32_t>(R)));
+        const uint32_t wi = invmod_c(root_of_unity(32u));
         for (int x = 0; x < 32; x++)
-            (*tab)[off + x] = x < R ? balanced(powmod_c(wi, static_cast<uint32_t>(x))) : 0;
+            (*tab)[off + x] = balanced(powmod_c(wi, static_cast<uint32_t>(x)));
     }
     off += 32;
     if (tab)

@@ -35,6 +35,11 @@ def xf_plan(N):
     return lgr, sh
 
 
+def prow(p):
+    """ntt.hip prow: the image row of position p (one empty row per 32)."""
+    return p + (p >> 5)
+
+
 def xf_pos(plan, t):
     lgr, sh = plan
     p = 0
@@ -102,6 +107,38 @@ def test_plan_shapes(N):
     assert sum(lgr) == N.bit_length() - 1 and max(lgr) <= 5 and sh[-1] == 0
     assert sorted(xf_pos((lgr, sh), t) for t in range(N)) == list(range(N))
     assert all(xf_index((lgr, sh), xf_pos((lgr, sh), t)) == t for t in range(N))
+
+
+@pytest.mark.parametrize("N", [32, 64, 128, 256, 512, 1024, 2048])
+def test_image_rows_and_banks(N):
+    """lds_pass_body addresses element q of task (b, j) as prow(b + j) +
+    prow(q s): exact for every pass of the plan (no carry into bit 5).  And
+    where the unit pass has radix 32 (n = 1024, k1000), its tasks, 32 rows
+    apart, sit on distinct banks of the 64 x 4-byte LDS banks at every tile
+    width T = 8 .. 64; with a radix-8 / 16 unit pass (n = 2048 / 512) up to
+    4 / 2 tasks share banks -- the radix-32 unit-pass plan that avoids it
+    measured slower (profiles/r6_ab_notes.txt), so the check is limited to
+    radix-32 unit passes."""
+    lgr, sh = xf_plan(N)
+    for b, s in zip(lgr, sh):
+        R, S = 1 << b, 1 << s
+        L = R * S
+        for tt in range(N // R):
+            j = tt & (S - 1)
+            x = (tt >> s) * L + j
+            for q in range(R):
+                assert prow(x + q * S) == prow(x) + prow(q * S), (N, b, s, tt, q)
+    R = 1 << lgr[-1]
+    if R != 32:
+        return
+    for lgT in range(3, 7):
+        T = 1 << lgT
+        tasks = 64 // T
+        for t0 in range(0, N // R, tasks):
+            for q in range(R):
+                banks = {((prow((t0 + i) * R + q) << lgT) + c) % 64
+                         for i in range(min(tasks, N // R - t0)) for c in range(T)}
+                assert len(banks) == min(tasks, N // R - t0) * T, (N, T, t0, q)
 
 
 @pytest.mark.parametrize("N", [4, 32, 64, 256, 512])
@@ -252,7 +289,11 @@ def test_erasure_decode_math(n, k, sys_):
     # passes, n = R0 R1): the unit pass of the zero-filled codeword plus its
     # response to c_E, then the last pass alone
     lg = n.bit_length() - 1
-    lg0 = (lg + 1) // 2
+    # the kernel's two-pass plan (round 6: the unit pass R1 = 32 from n = 64
+    # on; one-pass plans do not take this completion, any split checks the
+    # identity)
+    lgr, _ = xf_plan(n)
+    lg0 = lgr[0] if len(lgr) == 2 else (lg + 1) // 2
     R0, R1 = 1 << lg0, 1 << (lg - lg0)
     w1i = pow(ri, R0, Q)  # w_R1^-1
     # unit pass: group g (elements t = g + R0 q), output u
