@@ -330,10 +330,12 @@ def parse_args(argv=None):
     ap.add_argument("--timed-events", action="store_true",
                     help="record the per-kernel HIP events on the timed steps "
                          "(default: on the last warmup steps)")
-    ap.add_argument("--ctx-stream", type=int, default=None, choices=(0, 1),
+    ap.add_argument("--ctx-stream", type=int, default=None, choices=(0, 1, 2),
                     help="build the decode contexts from the ids alone on a "
                          "second stream beside the encode (default: off, "
-                         "see CTX_STREAM)")
+                         "see CTX_STREAM); 2: that stream at the low and the "
+                         "encode / decode stream at the high priority, so the "
+                         "context blocks fill the encode's last round")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the cfg3 line the default (cfg2) run appends")
@@ -453,6 +455,7 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
     ev = []
     overlap = (cfg in CTX_STREAM) if ctx_stream is None else bool(ctx_stream)
     overlap = overlap and NC == 1 and not dry
+    prio = overlap and ctx_stream == 2
 
     if dry:
         # the same loop structure on a small CPU stand-in per step
@@ -487,10 +490,12 @@ def run_config(cfg, stripes, sys_, steps, warmup, NC=1, n_streams=2, dist=None,
         # `streams` HIP streams, so one slice's encode (write-heavy) overlaps
         # another's decode (read-heavy); every slice is still encoded,
         # erased and decoded inside the timed step
-        streams = ([torch.cuda.current_stream()] if NC == 1 else
+        lo_p, hi_p = torch.cuda.Stream.priority_range() if prio else (0, 0)
+        streams = ([torch.cuda.Stream(priority=hi_p)] if prio else
+                   [torch.cuda.current_stream()] if NC == 1 else
                    [torch.cuda.Stream() for _ in range(max(1, n_streams))])
         cstride = plan.ctx_bytes(1, P)
-        cst = torch.cuda.Stream() if overlap else None
+        cst = torch.cuda.Stream(priority=lo_p) if overlap else None
 
         def step(timed):
             for j in range(NC):

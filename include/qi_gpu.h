@@ -126,9 +126,11 @@ int qi_gpu_decode_ctx(qi_plan* plan, const uint16_t* d_ids,
  * The context is not const in effect: a decode whose rows the matrix cores
  * cannot address fills the context's lazily built sections (the dot2
  * kernel's packed rows for k <= 256, the NTT engine's half for 256 < k <=
- * 640) the first time, on `stream`, and records that in the context.  So a
- * context may serve any number of decodes on one stream, but must not be
- * used by decodes on two streams at once. */
+ * 640) the first time, on `stream`, and records that in the context.  Every
+ * word such a fill writes gets the value it already holds when the section
+ * was filled before, so a context may serve any number of decodes, on one
+ * stream or on several at once (two decodes may then both fill it), once
+ * the qi_gpu_decode_ctx call that built it is ordered before them. */
 int qi_gpu_decode(qi_plan* plan, const void* d_ctx, const uint16_t* d_ids,
                   const uint16_t* d_data, long long dss, long long drs,
                   const uint16_t* d_coded, long long css, long long crs,
