@@ -53,9 +53,9 @@ int qi_gpu_device_count(void);
  *     multiple of 1024 columns and whose rows are 8-byte aligned inside
  *     31-bit buffer ranges (the encode only while the generator stays small:
  *     k * n_outputs <= 2^21, 2^18 systematic); the NTT engine otherwise;
- *   - 384 < k <= 640, non-systematic, n - k > 64: the decode as above on
- *     the matrix cores (k x k contexts, two K chunks); the encode, and every
- *     other batch, on the NTT engine;
+ *   - 384 < k <= 640, n - k > 64: the decode as above on the matrix cores
+ *     (k x k contexts, two K chunks); the encode, and every other batch, on
+ *     the NTT engine;
  *   - k > 384 otherwise: the NTT engine (column-batched NTT passes in LDS or
  *     HBM; the erasure decode when n - k <= 64). */
 qi_plan* qi_plan_create(int k, int m, int systematic);
@@ -104,7 +104,7 @@ size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
  * reads the marks from them directly (slightly slower per tile than routed
  * tables).  Built on the device, asynchronously on `stream`, for every k:
  * matrix contexts (the interpolation matrix, up to ~780 KB per stripe at
- * k = 256) for k <= 256, and for 256 < k <= 384 (non-systematic: 640) at widths that are a
+ * k = 256) for k <= 256, and for 256 < k <= 640 at widths that are a
  * multiple of 1024 columns (then followed by the NTT engine's context, used
  * when the decode's rows are not addressable by the matrix cores); the NTT
  * decode's per-pattern constants (src/fec_context.h:232-274, whose decode

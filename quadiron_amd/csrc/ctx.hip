@@ -383,19 +383,6 @@ __device__ __forceinline__ void pack_tiles_pass(int rb0, const Ent& ent, const u
     }
 }
 
-template <int NT>
-__device__ __forceinline__ void pack_tiles_direct(const uint32_t* Mt, int kp, const uint32_t* cinv,
-                                  const MatLayout& L, int32_t* mat, uint32_t* stg)
-{
-    auto ent = [&](int t, int i0, uint32_t (&e)[4]) {
-#pragma unroll
-        for (int jb = 0; jb < 4; jb++)
-            e[jb] = i0 + jb < L.kin ? Mt[static_cast<size_t>(t) * kp + i0 + jb] : 0u;
-    };
-    for (int rb0 = 0; rb0 < L.RB(); rb0 += 2)
-        pack_tiles_pass<NT, 32>(rb0, ent, cinv, L, mat, stg);
-}
-
 // LDS row pitch of the context kernel's k x k matrix: 4 x odd, >= k
 __host__ __device__ inline int ctx_pitch(int k)
 {
@@ -419,8 +406,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     // reads 16 rows x 16 bytes per wave (ds_read_b128) conflict-free (the
     // odd pitch k | 1 had SQ_LDS_BANK_CONFLICT at 7.4 cycles per LDS
     // instruction at k = 64)
-    // nb blocks per stripe (the non-systematic whole-tile form only; nb = 1
-    // otherwise): block cb builds the row chunks [c0, c1) of its stripe's
+    // nb blocks per stripe (the whole-tile forms only; nb = 1 otherwise):
+    // block cb builds the row chunks [c0, c1) of its stripe's
     // matrix, block 0 also the ids and the route table; each computes A(x)
     // and the A'(x_i) itself (few stripes per launch left most CUs idle
     // behind one block per stripe: k300, 32 stripes, 147 us)
@@ -696,7 +683,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
         if (ap == 0u)  // repeated ids
             atomicOr(err, kErrBadIds);
     }
-    if (mode != 0) {
+    if (mode != 0 && !(BIG && !dot2)) {
         // systematic: M[t][i] = Q_i(r^t) / A'(x_i), one thread per row t,
         // with Q_i(r^t) = A(r^t) / (r^t - x_i): 0 when r^t is another
         // received point (A(r^t) = 0), A'(x_i) when it is x_i itself.  The
@@ -732,34 +719,76 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     __syncthreads();
     if constexpr (BIG) {
         uint32_t* stg = big_lds;  // the tree's buffers are dead now
-        if (!dot2 && mode == 0) {
-            // whole-tile widths, non-systematic: the rows in 64-row chunks
-            // from the top, never in global memory.  Thread i runs Q_i's
-            // synthetic division again (1 / A'(x_i) is known now), writing
-            // the chunk's rows into LDS; then the chunk's two row blocks are
-            // packed straight into the operand tiles (32 lanes per row, 4
-            // entries per lane and group: scale, split, staged, stored
+        if (!dot2) {
+            // whole-tile widths: the rows in chunks of CH (ctx_chunk), this
+            // block's chunks [c0, c1) of the stripe's nb blocks, never in
+            // global memory: each chunk's rows written into LDS, then its row
+            // blocks packed straight into the operand tiles (LPR lanes per
+            // row, 4 entries per lane and group: scale, split, staged, stored
             // rows-fastest as whole tile lines).  No `plain` rows, no dot2
             // section (the kernels take single coefficients from the tiles).
+            //   non-systematic: thread i runs Q_i's synthetic division again
+            // (1 / A'(x_i) is known now), from the top down through the rows
+            // above the block's chunks without keeping them.
+            //   systematic: row t is Q_i(r^t) = A(r^t) / (r^t - x_i), or
+            // A'(x_i) where r^t = x_i (the packing applies the column scale
+            // 1 / A'(x_i)).  TPR lanes per row: each evaluates a segment of A's
+            // k + 1 coefficients at r^t (the segments summed across the group
+            // by shuffles) and inverts a seg-entry slice of the row's r^t - x_i
+            // at once (prefix products, one inversion, walked back).  (One
+            // thread per row, the rows through `plain`, one block per stripe:
+            // k600 systematic context 0.99 ms at 16 stripes.)
             uint32_t* ch = qi_ctx_lds;  // CH x kpc
             const int CH = ctx_chunk(k);
             const int kpc = (k + 3) & ~3;
-            const int32_t xi = tid < k ? balanced(xs[tid]) : 0;
-            const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
-            // this block's chunks [c0, c1): the division runs down from the
-            // top through the rows above them without keeping them
             const int nch = (k + CH - 1) / CH;
             const int c0 = (cb * nch + nb - 1) / nb, c1 = ((cb + 1) * nch + nb - 1) / nb;
+            const int32_t* Ab = reinterpret_cast<const int32_t*>(A);
+            const int32_t xi = tid < k ? balanced(xs[tid]) : 0;
             int32_t q = 1;  // coef_{k-1}(Q_i)
-            if (tid < k)
+            if (mode == 0 && tid < k)
                 q = div_steps(Ab, xi, q, k - 2, CH * c1, [](int, int32_t) {});
+            const int TPR = NT / CH;  // 16 or 32: a row's lanes share a wave
             for (int c = c1 - 1; c >= c0; c--) {
                 const int lo = CH * c, hi = min(k, lo + CH);
-                if (tid < k) {
-                    auto keep = [&](int t, int32_t qt) { ch[(t - lo) * kpc + tid] = canon_lz(qt); };
-                    if (hi == k)
-                        keep(k - 1, q);
-                    q = div_steps(Ab, xi, q, hi == k ? k - 2 : hi - 1, lo, keep);
+                if (mode == 0) {
+                    if (tid < k) {
+                        auto keep = [&](int t, int32_t qt) {
+                            ch[(t - lo) * kpc + tid] = canon_lz(qt);
+                        };
+                        if (hi == k)
+                            keep(k - 1, q);
+                        q = div_steps(Ab, xi, q, hi == k ? k - 2 : hi - 1, lo, keep);
+                    }
+                } else if (lo + tid / TPR < k) {  // uniform in the row's lane group
+                    const int sub = tid % TPR, rl = tid / TPR, t = lo + rl;
+                    const int len = (k + TPR) / TPR;      // ceil((k + 1) / TPR)
+                    const int seg = (k + TPR - 1) / TPR;  // ceil(k / TPR)
+                    const uint32_t et = powm(r, static_cast<uint32_t>(t));
+                    const int j0 = sub * len, j1 = min(k + 1, j0 + len);
+                    uint32_t term = 0;
+                    if (j0 < j1) {
+                        // sum_{j0 <= j < j1} A[j] (r^t)^(j - j0), times (r^t)^j0
+                        const int32_t h = div_steps(Ab - 1, balanced(et), 0, j1 - 1, j0,
+                                                    [](int, int32_t) {});
+                        term = mulm(canon_lz(fold(h)), powm(et, static_cast<uint32_t>(j0)));
+                    }
+                    const uint32_t av = grp_add(term, TPR) % 65537u;  // A(r^t)
+                    uint32_t* row = ch + rl * kpc;
+                    const int i0 = sub * seg, i1 = min(k, i0 + seg);
+                    uint32_t pre = 1;
+                    for (int i = i0; i < i1; i++) {
+                        const uint32_t d = subm(et, xs[i]);
+                        row[i] = pre;
+                        pre = mulm(pre, d ? d : 1u);
+                    }
+                    uint32_t inv = powm(pre, 65535u);
+                    for (int i = i1 - 1; i >= i0; i--) {
+                        const uint32_t d = subm(et, xs[i]);
+                        const uint32_t inv_i = mulm(inv, row[i]);
+                        inv = mulm(inv, d ? d : 1u);
+                        row[i] = d ? mulm(av, inv_i) : aprime[i];
+                    }
                 }
                 __syncthreads();
                 auto ent = [&](int t, int i0, uint32_t (&e)[4]) {
@@ -769,17 +798,12 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                     e[2] = v.z;
                     e[3] = v.w;
                 };
-                // (ends with a barrier)
+                // (ends with a barrier: the chunk buffer is free again)
                 if (CH == kCtxChunk)
                     pack_tiles_pass<NT, NT / kCtxChunk>(lo >> 4, ent, cinv, L, mat, stg);
                 else
                     pack_tiles_pass<NT, NT / 32>(lo >> 4, ent, cinv, L, mat, stg);
             }
-            return;
-        }
-        if (!dot2) {
-            // systematic: the rows were built in `plain` (global) above
-            pack_tiles_direct<NT>(Mt, kp, cinv, L, mat, stg);
             return;
         }
     }
@@ -1318,12 +1342,11 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
         // the matrix rows in the context itself (no LDS image); 1024 threads
         // keep 4x more of the packing and tile passes' row loads in flight
         // (k256 decode 0.81 -> 0.77 ms, k200 2.09 -> 2.05 ms)
-        // (only the non-systematic whole-tile contexts stage kCtxChunk-row
-        // chunks of the matrix in the dynamic LDS; the systematic and dot2
-        // forms keep the rows in global memory and reserve none)
-        const size_t lds = mode == 0 && !dot2
-                               ? static_cast<size_t>(ctx_chunk(k)) * ((k + 3) & ~3) * 4
-                               : 0;
+        // (the whole-tile contexts stage ctx_chunk(k)-row chunks of the
+        // matrix in the dynamic LDS; the dot2 forms keep the rows in global
+        // memory and reserve none)
+        const size_t lds =
+            !dot2 ? static_cast<size_t>(ctx_chunk(k)) * ((k + 3) & ~3) * 4 : 0;
         static std::atomic<uint64_t> attr_done{0};
         static std::atomic<int> cus_of[64];
         int dev = 0;
@@ -1352,10 +1375,10 @@ int launch_decode_ctx(int k, int n, uint32_t r, int mode, const MatLayout& L,
                 return -2;
             attr_done.fetch_or(bit, std::memory_order_release);
         }
-        // the non-systematic whole-tile form splits a stripe's row chunks
-        // over up to (CUs / stripes) blocks (one block per CU each)
+        // the whole-tile forms split a stripe's row chunks over up to (CUs /
+        // stripes) blocks (one block per CU each)
         int nb = 1;
-        if (mode == 0 && !dot2) {
+        if (!dot2) {
             const int cus = bit ? cus_of[dev].load(std::memory_order_relaxed) : 256;
             const int nch = (k + ctx_chunk(k) - 1) / ctx_chunk(k);
             nb = std::max(1, std::min(nch, cus / S));

@@ -1903,7 +1903,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     using O = OsTile<KC, WR>;  // one chunk's image (the whole K when NCH = 1)
     constexpr int KH = O::kRows, RSB = O::kPitch, RPT = O::kRpt, NCOL = O::kCols;
     static_assert(KS % 4 == 0 && KC % 4 == 0, "x64 pairs with zero halves");
-    static_assert(NCH == 1 || (RPW == 1 && !TWO), "K chunks: one row block per wave, one region");
+    static_assert(NCH == 1 || RPW == 1, "K chunks: one row block per wave");
     extern __shared__ __attribute__((aligned(16))) uint8_t qi_lds[];
     const MatLayout L = a.L;
     const RowSrc src = a.src;
@@ -2015,8 +2015,13 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     const Region<true> go(dst.base + s * dst.ss, ext.eo);
     const int rowgrp = tid / O::kTpr, cl = (tid % O::kTpr) * 4;
     constexpr uint32_t kOob = 0x80000000u;  // past any extent (< 2^31)
-    // (chunk c stages the received rows KH c .. KH c + KH - 1)
-    uint32_t off0[NCH][RPT], off1[TWO ? RPT : 1];
+    // (chunk c stages the received rows KH c .. KH c + KH - 1).  TWO with K
+    // chunks (384 < k <= 640 systematic): one offset per row, in its own
+    // region, and bit c RPT + r of rgn set for rows of region 1 (a second
+    // offset array would not fit the registers)
+    constexpr bool TWO1 = TWO && NCH == 1, TWOC = TWO && NCH > 1;
+    static_assert(NCH * RPT <= 32, "region bits");
+    uint32_t off0[NCH][RPT], off1[TWO1 ? RPT : 1], rgn = 0;
 #pragma unroll
     for (int c = 0; c < NCH; c++)
 #pragma unroll
@@ -2025,10 +2030,16 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             const int ii = i < kin ? i : kin - 1;
             const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
             const uint32_t lane = static_cast<uint32_t>(cl * 2);
-            if constexpr (TWO) {
+            if constexpr (TWO1) {
                 const bool lo = id < src.split;
                 off0[c][r] = lo ? static_cast<uint32_t>(id * src.rs0 * 2) + lane : kOob;
                 off1[r] = lo ? kOob : static_cast<uint32_t>((id - src.split) * src.rs1 * 2) + lane;
+            } else if constexpr (TWOC) {
+                const bool lo = id < src.split;
+                off0[c][r] = (lo ? static_cast<uint32_t>(id * src.rs0 * 2)
+                                 : static_cast<uint32_t>((id - src.split) * src.rs1 * 2)) +
+                             lane;
+                rgn |= (lo ? 0u : 1u) << (c * RPT + r);
             } else {
                 off0[c][r] = static_cast<uint32_t>(id * src.rs0 * 2) + lane;
             }
@@ -2050,13 +2061,17 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         const uint32_t oob = valid ? 0u : kOob;
 #pragma unroll
         for (int r = 0; r < RPT; r++) {
+            // (TWOC: the row's offset in one region, past the extent in the
+            // other; the hardware returns zeros there)
+            const bool in1 = TWOC && ((rgn >> (c * RPT + r)) & 1u);
             const auto v = __builtin_amdgcn_raw_buffer_load_b64(
-                g0.r, static_cast<int>(off0[c][r] | oob), so, kAuxLdOs);
+                g0.r, static_cast<int>(in1 ? kOob : (off0[c][r] | oob)), so, kAuxLdOs);
             wr[r][0] = v[0];
             wr[r][1] = v[1];
             if constexpr (TWO) {
+                const uint32_t o1 = TWOC ? (in1 ? (off0[c][r] | oob) : kOob) : (off1[r] | oob);
                 const auto u = __builtin_amdgcn_raw_buffer_load_b64(
-                    g1.r, static_cast<int>(off1[r] | oob), so, kAuxLdOs);
+                    g1.r, static_cast<int>(o1), so, kAuxLdOs);
                 wr[r][0] |= u[0];
                 wr[r][1] |= u[1];
             }
@@ -2672,8 +2687,8 @@ template <int KS, int WR, int RPW>
 static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 {
     using O = OsTile<OsK<KS>::KC, WR>;
-    // the systematic decodes' two source regions: KS <= 24 only (os_geom)
-    constexpr bool kTwo = RPW == 1 && OsK<KS>::NCH == 1;
+    // the systematic decodes' two source regions (os_geom: RPW = 1)
+    constexpr bool kTwo = RPW == 1;
     const long long TS = wfull / O::kCols;
     if (TS <= 0 || TS > 0x7fffffffLL)
         return -1;
@@ -2783,10 +2798,10 @@ inline OsGeom os_geom(int KS, int RB, bool two)
     // gpurun_out/ab_r5k, ab_r5l)
     if ((KS == 16 || KS == 20 || KS == 24) && RB > 8 && !two)
         return {8, 2};
-    // KS = 40 (384 < k <= 640, K chunks): non-systematic decodes only, one
-    // row block per wave (80 operand VGPRs)
+    // KS = 40 (384 < k <= 640, K chunks): one row block per wave (80
+    // operand VGPRs), one or two source regions
     if (KS > 24)
-        return two ? OsGeom{0, 0} : OsGeom{8, 1};
+        return {8, 1};
     if (KS >= 8)
         return {8, 1};
     // KS = 4: the short decode matrices (2 super tiles per 128-column tile)

@@ -189,13 +189,10 @@ qi_plan* qi_plan_create_ex(int k, int m, int systematic, int flags)
         // (qi_gpu.cpp use_matrix: words a multiple of 1024), with the
         // generator below and per-stripe k x k contexts
         p->ntt = 1;
-        // 384 < k <= 640: the non-systematic decodes on the matrix cores
-        // (KS = 40, two K chunks), unless the code misses few symbols (the
-        // erasure decode's O(e^2 + n log n) per column beats O(k^2))
-        p->mbig = k <= kMatGenMaxKin ||
-                          (k <= kMatMaxKin && !p->sys && !eras_shape(k, p->n))
-                      ? 1
-                      : 0;
+        // 384 < k <= 640: the decodes on the matrix cores (KS = 40, two K
+        // chunks), unless the code misses few symbols (the erasure decode's
+        // O(e^2 + n log n) per column beats O(k^2))
+        p->mbig = k <= kMatGenMaxKin || (k <= kMatMaxKin && !eras_shape(k, p->n)) ? 1 : 0;
         ok = ntt_plan_init(p) == 0;
     }
     if (ok && (!p->ntt || p->mbig)) {

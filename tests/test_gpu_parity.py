@@ -355,13 +355,17 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True,
     (321, 63, 0, 2, 1024),    # KS = 24
     (384, 128, 0, 1, 2048),   # largest generator / systematic matrix-path k
     (384, 100, 1, 1, 1024),
-    # 384 < k <= 640, non-systematic, n - k > 64, whole 1024-column tiles:
-    # the decode on the matrix cores at KS = 40 in two K chunks (round 6;
-    # the encode stays on the NTT engine)
+    # 384 < k <= 640, n - k > 64, whole 1024-column tiles: the decode on the
+    # matrix cores at KS = 40 in two K chunks (round 6; the encode stays on
+    # the NTT engine); systematic: the two source regions, the mode-1
+    # contexts' rows through global memory
     (385, 127, 0, 2, 1024),   # smallest KS = 40 code
     (500, 524, 0, 1, 2048),
     (600, 1400, 0, 1, 1024),  # the k600 bench code
     (640, 384, 0, 1, 1024),   # largest matrix-path k
+    (385, 127, 1, 2, 1024),
+    (600, 1400, 1, 1, 1024),
+    (640, 384, 1, 1, 2048),
     # k > 256: the NTT-structured general path (ntt.hip)
     (257, 255, 0, 1, 300),    # smallest NTT-path code
     (300, 100, 1, 1, 300),    # systematic: interpolation + NTT_n encode
@@ -555,6 +559,7 @@ def test_decode_row_scales_many_stripes(k, m, S, P):
 
 @pytest.mark.parametrize("k,m,sys_", [
     (300, 100, 0), (300, 100, 1),   # 256 < k <= 384: the NTT engine takes them
+    (500, 524, 0), (500, 524, 1),   # 384 < k <= 640 (KS = 40 plans): the same
     (16, 48, 0), (64, 960, 0), (200, 56, 1),  # the dot2 kernel, its context
                                               # sections filled from the tiles
 ])
