@@ -389,6 +389,42 @@ __host__ __device__ inline int ctx_pitch(int k)
     return (k + 3) / 8 * 8 + 4;
 }
 
+// The received fragments of stripe s in the context's order: for the
+// systematic decodes (part) the data fragments (id < k) first, then the
+// parity ones, each in the caller's order (a stable partition from ballot
+// counts), so that the matrix kernels' two source regions meet at one
+// position (matrix_os_kernel: one load per row).  The matrix columns, the
+// route entries and the ids the decode reads (cids) all follow this order;
+// identity otherwise.  NT threads, k <= NT; pid and wtot (NT / 64) in LDS.
+template <int NT>
+__device__ void order_ids(const uint16_t* sids, int k, bool part, uint16_t* pid, int* wtot)
+{
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint16_t id = tid < k ? sids[tid] : uint16_t{0};
+    if (!part) {  // block-uniform
+        if (tid < k)
+            pid[tid] = id;
+        __syncthreads();
+        return;
+    }
+    const bool lo = tid < k && id < k;
+    const uint64_t b = __ballot(lo);
+    const int before = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0)
+        wtot[w] = __popcll(b);
+    __syncthreads();
+    int pre = before, P = 0;
+#pragma unroll
+    for (int v = 0; v < NT / 64; v++) {
+        const int c = wtot[v];
+        P += c;
+        pre += v < w ? c : 0;
+    }
+    if (tid < k)
+        pid[lo ? pre : P + (tid - pre)] = id;
+    __syncthreads();
+}
+
 template <int NT, bool BIG>
 __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     int k, int n, uint32_t r, int mode, MatLayout L, const uint16_t* __restrict__ ids,
@@ -399,6 +435,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     __shared__ uint32_t A[kMatMaxKin + 1];
     __shared__ uint32_t cinv[kMatMaxKin];    // 1 / A'(x_i)
     __shared__ uint32_t aprime[kMatMaxKin];  // A'(x_i)
+    __shared__ uint16_t pid[kMatMaxKin];     // the ids in the context's order
+    __shared__ int wtot[NT / 64];
     // k x k matrix, sized by the launch: 1 KiB at k = 16 instead of a fixed 32 KiB, which had
     // limited the kernel to 4 workgroups per CU
     extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
@@ -439,8 +477,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             route[lazy_word_off(words)] = 0;  // no lazily filled section yet
         }
     }
+    order_ids<NT>(ids + static_cast<long long>(s) * k, k, mode != 0 && !by_pos, pid, wtot);
     if (tid < k) {
-        const uint32_t id = ids[static_cast<long long>(s) * k + tid];
+        const uint32_t id = pid[tid];
         xs[tid] = powm(r, id);
         if (lead) {
             cids[tid] = static_cast<int32_t>(id);
@@ -454,7 +493,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (lead && in_oor.counts && tid < k) {
-        const int id = ids[static_cast<long long>(s) * k + tid];
+        const int id = pid[tid];
         const int slot = (by_pos ? tid : id) - slot_base;
         // rows outside the bucket array (systematic data rows below
         // slot_base; bad ids past it) have no marks here
@@ -937,6 +976,8 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
     __shared__ int32_t A[129];        // balanced coefficients of A(x)
     __shared__ __attribute__((aligned(16))) uint32_t cinv[128];  // 1 / A'(x_i)
     __shared__ uint32_t aprime[128];  // A'(x_i)
+    __shared__ uint16_t pid[128];     // the ids in the context's order
+    __shared__ int wtot[NT / 64];
     extern __shared__ __attribute__((aligned(16))) uint32_t qi_ctx_lds[];
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
@@ -966,11 +1007,12 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         }
         __builtin_amdgcn_s_waitcnt(0);  // this wave's clears before its atomics
     }
+    order_ids<NT>(ids + static_cast<long long>(s) * k, k, mode != 0 && !by_pos, pid, wtot);
     // x_i = r^{id_i}: thread tid takes point tid (its Q chain below); wave 0
     // also point 64 + lane (its A(x) chain reads every point by readlane)
     int32_t xt = 0, xt1 = 0;
     if (tid < k) {
-        const uint32_t id = ids[static_cast<long long>(s) * k + tid];
+        const uint32_t id = pid[tid];
         xt = balanced(canon_lz(rpow_lz(rp, id, lgn)));
         xs[tid] = static_cast<uint32_t>(xt < 0 ? xt + kQ : xt);
         cids[tid] = static_cast<int32_t>(id);
@@ -978,7 +1020,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
             atomicOr(err, kErrBadIds);
     }
     if (tid < 64 && 64 + tid < k)
-        xt1 = balanced(canon_lz(rpow_lz(rp, ids[static_cast<long long>(s) * k + 64 + tid], lgn)));
+        xt1 = balanced(canon_lz(rpow_lz(rp, pid[64 + tid], lgn)));
     int32_t ab0 = 0;  // wave 0: balanced A[lane] (k <= 64), for the Q chains
     if (tid < 64) {
         // A(x) = prod_i (x - x_i): lane d holds coefficient d (a0) and
@@ -1015,7 +1057,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         // other waves, while wave 0 builds A(x)): every row's marks, each
         // wave adding those of its own tiles
         for (int i = rl; i < k; i += 64) {
-            const int id = ids[static_cast<long long>(s) * k + i];
+            const int id = pid[i];
             const int slot = (by_pos ? i : id) - slot_base;
             if (slot < 0 || slot >= in_oor.slots)
                 continue;

@@ -2007,21 +2007,27 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
 
     // staging: lane (rowgrp, cl) loads 4 columns (b64) of rows kRpp r +
     // rowgrp; per-lane row offsets fixed for the block (rows past kin
-    // clamped: their operand bytes are 0).  TWO (two source regions,
-    // systematic decodes): both regions are loaded, with an out-of-range
-    // offset in the region the row is not in (the hardware returns 0).
+    // clamped: their operand bytes are 0); chunk c stages the received rows
+    // KH c .. KH c + KH - 1.
+    //   TWO (two source regions, the systematic decodes): one offset per
+    // row, in its own region.  The context lists the received rows region by
+    // region (order_ids, ctx.hip), so a wave's load of pass (c, r) reads one
+    // region, through that region's descriptor (bit c RPT + r of sel), but
+    // for at most one pass (xcr) that straddles the boundary: its region-1
+    // lanes take an extra load (wx, one per item, past the extent in every
+    // other item: zeros), ORed into that row when it is written to LDS.
+    // (Each row loaded through both descriptors, past the extent in the
+    // other region, took the k600 systematic decode 1.11 -> 1.92 ms:
+    // twice the load instructions, gpurun_out/r6l.)
     const Region<true> g0(src.base0 + s * src.ss0, ext.e0);
     const Region<true> g1(src.base1 ? src.base1 + s * src.ss1 : src.base0, ext.e1);
     const Region<true> go(dst.base + s * dst.ss, ext.eo);
     const int rowgrp = tid / O::kTpr, cl = (tid % O::kTpr) * 4;
     constexpr uint32_t kOob = 0x80000000u;  // past any extent (< 2^31)
-    // (chunk c stages the received rows KH c .. KH c + KH - 1).  TWO with K
-    // chunks (384 < k <= 640 systematic): one offset per row, in its own
-    // region, and bit c RPT + r of rgn set for rows of region 1 (a second
-    // offset array would not fit the registers)
-    constexpr bool TWO1 = TWO && NCH == 1, TWOC = TWO && NCH > 1;
-    static_assert(NCH * RPT <= 32, "region bits");
-    uint32_t off0[NCH][RPT], off1[TWO1 ? RPT : 1], rgn = 0;
+    static_assert(NCH * RPT <= 32, "pass bits");
+    uint32_t off0[NCH][RPT];
+    uint32_t sel = 0, offx = kOob;  // sel: wave-uniform
+    int xcr = -1;                   // wave-uniform: c RPT + r of the straddling pass
 #pragma unroll
     for (int c = 0; c < NCH; c++)
 #pragma unroll
@@ -2030,20 +2036,27 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             const int ii = i < kin ? i : kin - 1;
             const int id = src.by_pos ? ii : (sid ? sid[ii] : ii);
             const uint32_t lane = static_cast<uint32_t>(cl * 2);
-            if constexpr (TWO1) {
-                const bool lo = id < src.split;
-                off0[c][r] = lo ? static_cast<uint32_t>(id * src.rs0 * 2) + lane : kOob;
-                off1[r] = lo ? kOob : static_cast<uint32_t>((id - src.split) * src.rs1 * 2) + lane;
-            } else if constexpr (TWOC) {
+            if constexpr (TWO) {
                 const bool lo = id < src.split;
                 off0[c][r] = (lo ? static_cast<uint32_t>(id * src.rs0 * 2)
                                  : static_cast<uint32_t>((id - src.split) * src.rs1 * 2)) +
                              lane;
-                rgn |= (lo ? 0u : 1u) << (c * RPT + r);
+                const uint64_t b1 = __ballot(!lo);
+                if (b1 == ~0ull) {
+                    sel |= 1u << (c * RPT + r);
+                } else if (b1 != 0ull) {
+                    if (xcr >= 0 && a.err && l == 0)
+                        atomicOr(a.err, kErrBadIds);  // rows not in region order
+                    xcr = c * RPT + r;
+                    offx = lo ? kOob : off0[c][r];
+                }
             } else {
                 off0[c][r] = static_cast<uint32_t>(id * src.rs0 * 2) + lane;
             }
         }
+    sel = __builtin_amdgcn_readfirstlane(sel);
+    xcr = __builtin_amdgcn_readfirstlane(xcr);
+    const int xc = xcr >= 0 ? xcr / RPT : -1, xr = xcr >= 0 ? xcr % RPT : -1;
     // DEEP (KS = 4, the short decodes): ND tiles of rows in flight per
     // block (a ring of ND register sets, 8 VGPRs each) -- with one, a CU
     // kept ~32 KB of loads in flight and the cfg3 decode was bound by the
@@ -2052,45 +2065,55 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
     constexpr int ND = KS == 4 ? 2 : 1;
     constexpr bool DEEP = ND >= 2;
     uint32_t w[RPT][2], wring[DEEP ? ND : 1][DEEP ? RPT : 1][2];
+    uint32_t wx[2], wxring[DEEP ? ND : 1][2];  // TWO: the straddling pass's region-1 lanes
     // rows of `tile` into wr; an invalid tile (past the block's range) loads
     // from past the buffer's extent (no memory access, zeros), so the number
     // of loads in flight is the same on every path
-    auto issue_rows_to = [&](int tile, bool valid, auto& wr, auto cc) {
+    auto issue_rows_to = [&](int tile, bool valid, auto& wr, auto& wxr, auto cc) {
         constexpr int c = decltype(cc)::value;  // K chunk
         const int so = valid ? tile * NCOL * 2 : 0;  // byte offset of the tile's first column
         const uint32_t oob = valid ? 0u : kOob;
 #pragma unroll
         for (int r = 0; r < RPT; r++) {
-            // (TWOC: the row's offset in one region, past the extent in the
-            // other; the hardware returns zeros there)
-            const bool in1 = TWOC && ((rgn >> (c * RPT + r)) & 1u);
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(
-                g0.r, static_cast<int>(in1 ? kOob : (off0[c][r] | oob)), so, kAuxLdOs);
+            uint32_t o = off0[c][r] | oob;
+            auto rsrc = g0.r;
+            if constexpr (TWO) {
+                // (the straddling pass: its region-1 lanes through wx)
+                o = c * RPT + r == xcr && offx != kOob ? kOob : o;
+                rsrc = (sel >> (c * RPT + r)) & 1u ? g1.r : g0.r;
+            }
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, static_cast<int>(o), so,
+                                                                kAuxLdOs);
             wr[r][0] = v[0];
             wr[r][1] = v[1];
-            if constexpr (TWO) {
-                const uint32_t o1 = TWOC ? (in1 ? (off0[c][r] | oob) : kOob) : (off1[r] | oob);
-                const auto u = __builtin_amdgcn_raw_buffer_load_b64(
-                    g1.r, static_cast<int>(o1), so, kAuxLdOs);
-                wr[r][0] |= u[0];
-                wr[r][1] |= u[1];
-            }
+        }
+        if constexpr (TWO) {
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(
+                g1.r, static_cast<int>(c == xc ? offx | oob : kOob), so, kAuxLdOs);
+            wxr[0] = u[0];
+            wxr[1] = u[1];
         }
     };
     using C0 = std::integral_constant<int, 0>;
-    auto issue_rows = [&](int tile, auto cc) { issue_rows_to(tile, true, w, cc); };
+    auto issue_rows = [&](int tile, auto cc) { issue_rows_to(tile, true, w, wx, cc); };
     const uint32_t lpos = 64 * (cl / 64) + 16 * ((cl % 16) / 4) + 4 * ((cl % 64) / 16);
-    auto write_rows_from = [&](uint8_t* img, const auto& w) {
+    auto write_rows_from = [&](uint8_t* img, const auto& w, const auto& wxr) {
 #pragma unroll
         for (int r = 0; r < RPT; r++) {
             const int i = O::kRpp * r + rowgrp;
-            const uint32_t hi = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x07050301u) ^ 0x80808080u;
-            const uint32_t lo = __builtin_amdgcn_perm(w[r][1], w[r][0], 0x06040200u) ^ 0x80808080u;
+            uint32_t w0 = w[r][0], w1 = w[r][1];
+            if constexpr (TWO) {
+                // (zeros unless this item's chunk holds the straddling pass)
+                w0 |= r == xr ? wxr[0] : 0u;
+                w1 |= r == xr ? wxr[1] : 0u;
+            }
+            const uint32_t hi = __builtin_amdgcn_perm(w1, w0, 0x07050301u) ^ 0x80808080u;
+            const uint32_t lo = __builtin_amdgcn_perm(w1, w0, 0x06040200u) ^ 0x80808080u;
             *reinterpret_cast<uint32_t*>(img + i * RSB + lpos) = hi;
             *reinterpret_cast<uint32_t*>(img + (KH + i) * RSB + lpos) = lo;
         }
     };
-    auto write_rows = [&](uint8_t* img) { write_rows_from(img, w); };
+    auto write_rows = [&](uint8_t* img) { write_rows_from(img, w, wx); };
 
     // OOR marks of the received rows in a tile (route table or bucket
     // scan) into mark list mb; returns the count (all threads)
@@ -2319,8 +2342,8 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         // tiles t0 .. t0 + ND - 1 in flight, the first one into image 0
 #pragma unroll
         for (int d = 0; d < ND; d++)
-            issue_rows_to(t0 + d, t0 + d < t1, wring[d], C0{});
-        write_rows_from(img(0), wring[0]);
+            issue_rows_to(t0 + d, t0 + d < t1, wring[d], wxring[d], C0{});
+        write_rows_from(img(0), wring[0], wxring[0]);
         int nl[2];
         nl[0] = stage_marks(t0, 0);
         nl[1] = 0;
@@ -2331,7 +2354,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             constexpr int J = decltype(jc)::value;
             const int b = (tile - t0) & 1;
             const bool more = tile + 1 < t1;  // block-uniform
-            issue_rows_to(tile + ND, tile + ND < t1, wring[J], C0{});
+            issue_rows_to(tile + ND, tile + ND < t1, wring[J], wxring[J], C0{});
             const long long col0 = static_cast<long long>(tile) * NCOL + 64 * st;
             auto none = [] {};
             [&]<int... R>(std::integer_sequence<int, R...>) {
@@ -2345,7 +2368,7 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
             // compiler then drained vmcnt(0) before reusing the registers);
             // past the last tile it writes the invalid tile's zeros into an
             // image no wave reads again
-            write_rows_from(img(b ^ 1), wring[(J + 1) % ND]);
+            write_rows_from(img(b ^ 1), wring[(J + 1) % ND], wxring[(J + 1) % ND]);
             if (more)
                 nl[b ^ 1] = stage_marks(tile + 1, b ^ 1);
             __syncthreads();

@@ -19,11 +19,9 @@ RES = [os.path.join(ROOT, "build", "obj", f)
 # their 128-256 row ids are read from VGPR lanes instead of SGPRs)
 # Round 6: the k > 128 decode context (1024 threads, 128 VGPRs: a few values
 # kept across the chunk loop, 5 reloads per chunk; the non-systematic k300 /
-# k600 contexts measured 48 / 102 us either way, gpurun_out/r6k) and the
-# two-region KS = 40 kernel, whose spilled values are reloaded only on the
-# out-of-range marking path of the epilogue.
+# k600 contexts measured 48 / 102 us either way, gpurun_out/r6k).
 ALLOWED = ("matrix_redo_kernel", "encode_fnt_kernelILi64E",
-           "decode_ctx_kernelILi1024ELb1E", "matrix_os_kernelILi40ELi8ELi1ELb1E")
+           "decode_ctx_kernelILi1024ELb1E")
 
 
 def kernels():
