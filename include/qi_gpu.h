@@ -54,8 +54,9 @@ int qi_gpu_device_count(void);
  *     31-bit buffer ranges (the encode only while the generator stays small:
  *     k * n_outputs <= 2^21, 2^18 systematic); the NTT engine otherwise;
  *   - 384 < k <= 640, n - k > 64: the decode as above on the matrix cores
- *     (k x k contexts, two K chunks); the encode, and every other batch, on
- *     the NTT engine;
+ *     (k x k contexts, two K chunks), and the systematic encode while its
+ *     generator stays small (k * m <= 2^20); the non-systematic encode, and
+ *     every other batch, on the NTT engine;
  *   - k > 384 otherwise: the NTT engine (column-batched NTT passes in LDS or
  *     HBM; the erasure decode when n - k <= 64). */
 qi_plan* qi_plan_create(int k, int m, int systematic);

@@ -34,9 +34,10 @@ namespace qi {
 // decode 0.35 vs 0.62 ms.
 // the largest k the matrix kernels take (256 < k <= 640: whole 1024-column
 // tiles only, on the operand-stationary kernel; the NTT engine otherwise;
-// 384 < k <= 640: decodes only, KS = 40 in two K chunks)
+// 384 < k <= 640: the decodes and the systematic encodes, KS = 40 in two K
+// chunks)
 constexpr int kMatMaxKin = 640;
-// the largest k of the matrix-core encodes (KS <= 24)
+// the largest k of the non-systematic matrix-core encodes (KS <= 24)
 constexpr int kMatGenMaxKin = 384;
 
 struct MatLayout {

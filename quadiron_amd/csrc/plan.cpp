@@ -32,16 +32,18 @@ static bool enc_matrix(int K, int flags)
     return K >= 64;
 }
 
-// 256 < k <= 384: the matrix-core encode's generator (n_outputs x k,
+// 256 < k <= 640: the matrix-core encode's generator (n_outputs x k,
 // packed) is built only while it stays small; larger codes encode on the NTT
 // engine (a k = 384 generator for m near 65536 would take ~250 MB of device
-// memory and seconds of host time for the systematic Lagrange rows)
+// memory).  384 < k <= 640: systematic codes only (k600 systematic encode
+// on the NTT engine: interpolation + NTT_n, 6.1 ms per 16 stripes, about
+// 3x its non-systematic encode, which stays there)
 static bool big_generator_ok(int k, int n_outputs, int sys)
 {
-    if (k > kMatGenMaxKin)
-        return false;  // 384 < k <= 640: the matrix cores decode only
+    if (k > kMatMaxKin || (k > kMatGenMaxKin && !sys))
+        return false;
     const long long e = static_cast<long long>(k) * n_outputs;
-    return e <= (sys ? (1LL << 18) : (1LL << 21));
+    return e <= (sys ? (1LL << 20) : (1LL << 21));
 }
 
 static uint32_t addm(uint32_t a, uint32_t b)
@@ -70,26 +72,51 @@ std::vector<uint32_t> lagrange_matrix(int k, uint32_t r, const uint32_t* ids,
             A[d] = addm(A[d - 1], mulmod_c(A[d], neg));
         A[0] = mulmod_c(A[0], neg);
     }
+    std::vector<uint32_t> dinv(k);  // 1 / A'(x_i) = 1 / prod_{j != i} (x_i - x_j)
     for (int i = 0; i < k; i++) {
-        q[k - 1] = A[k];
-        for (int j = k - 1; j >= 1; j--)
-            q[j - 1] = addm(A[j], mulmod_c(x[i], q[j]));
         uint32_t den = 1;
         for (int j = 0; j < k; j++)
             if (j != i)
                 den = mulmod_c(den, subm(x[i], x[j]));
-        const uint32_t inv = invmod_c(den);
+        dinv[i] = invmod_c(den);
+    }
+    if (mode != 0) {
+        // evaluation rows: M[t][i] = Q_i(e_t) / A'(x_i) with Q_i(e_t) = A(e_t) /
+        // (e_t - x_i), or delta_ij where e_t = x_j; a row's k inverses from
+        // one inversion (prefix products walked back): O(R k) where a Horner
+        // of every Q_i at every e_t took O(R k^2) (seconds at k = 600, R =
+        // 1400)
+        std::vector<uint32_t> pre(k);
         for (int t = 0; t < R; t++) {
-            uint32_t v;
-            if (mode == 0) {
-                v = q[t];
-            } else {
-                v = 0;
-                for (int j = k - 1; j >= 0; j--)
-                    v = addm(mulmod_c(v, eval[t]), q[j]);
+            const uint32_t e = eval[t];
+            uint32_t ae = 0;  // A(e), A monic of degree k
+            for (int j = k; j >= 0; j--)
+                ae = addm(mulmod_c(ae, e), A[j]);
+            uint32_t acc = 1;
+            int hit = -1;
+            for (int i = 0; i < k; i++) {
+                const uint32_t d = subm(e, x[i]);
+                hit = d ? hit : i;
+                pre[i] = acc;
+                acc = mulmod_c(acc, d ? d : 1u);
             }
-            M[static_cast<size_t>(t) * k + i] = mulmod_c(v, inv);
+            uint32_t inv = invmod_c(acc);
+            uint32_t* row = M.data() + static_cast<size_t>(t) * k;
+            for (int i = k - 1; i >= 0; i--) {
+                const uint32_t d = subm(e, x[i]);
+                const uint32_t inv_i = mulmod_c(inv, pre[i]);
+                inv = mulmod_c(inv, d ? d : 1u);
+                row[i] = hit >= 0 ? (i == hit ? 1u : 0u) : mulmod_c(mulmod_c(ae, inv_i), dinv[i]);
+            }
         }
+        return M;
+    }
+    for (int i = 0; i < k; i++) {
+        q[k - 1] = A[k];
+        for (int j = k - 1; j >= 1; j--)
+            q[j - 1] = addm(A[j], mulmod_c(x[i], q[j]));
+        for (int t = 0; t < R; t++)
+            M[static_cast<size_t>(t) * k + i] = mulmod_c(q[t], dinv[i]);
     }
     return M;
 }

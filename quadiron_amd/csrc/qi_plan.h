@@ -87,8 +87,9 @@ struct qi_plan {
     int ntt = 0, len2k = 0, nmax = 0;
     // 256 < k <= 384: batches whose columns tile exactly (words a multiple
     // of 1024) run the matrix cores instead (d_gen, k x k contexts); also
-    // 384 < k <= 640, n - k > 64: the decodes only (no
-    // generator; the encode stays on the NTT engine)
+    // 384 < k <= 640, n - k > 64: the decodes, and the systematic encodes
+    // with a small generator (big_generator_ok; the non-systematic encodes
+    // stay on the NTT engine)
     int mbig = 0;
     int32_t* d_tw[2] = {nullptr, nullptr};
     int32_t* d_ldstw = nullptr;  // per-pass twiddle tables of the LDS engine
