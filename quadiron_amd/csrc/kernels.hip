@@ -2710,8 +2710,9 @@ template <int KS, int WR, int RPW>
 static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
 {
     using O = OsTile<OsK<KS>::KC, WR>;
-    // the systematic decodes' two source regions (os_geom: RPW = 1)
-    constexpr bool kTwo = RPW == 1;
+    // the systematic decodes' two source regions (not at KS = 24 with two
+    // row blocks per wave: 28 bytes of scratch; os_geom)
+    constexpr bool kTwo = !(KS >= 24 && RPW == 2);
     const long long TS = wfull / O::kCols;
     if (TS <= 0 || TS > 0x7fffffffLL)
         return -1;
@@ -2727,10 +2728,9 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
         return -2;
     const uint64_t bit = dev < 64 ? 1ull << dev : 0;
     if (!bit || !(attr_done.load(std::memory_order_acquire) & bit)) {
-        // (two source regions only at RPW = 1, os_geom)
         const void* two_fn = nullptr;
         if constexpr (kTwo)
-            two_fn = reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, 1, true>);
+            two_fn = reinterpret_cast<const void*>(&matrix_os_kernel<KS, WR, RPW, true>);
         if (lds > 65536 &&
             ((two_fn && hipFuncSetAttribute(two_fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             static_cast<int>(lds)) != hipSuccess) ||
@@ -2792,7 +2792,7 @@ static int os_launch(MatArgs a, long long wfull, int S, hipStream_t st)
         if constexpr (!kTwo)
             return -1;  // not chosen by os_geom
         else
-            hipLaunchKernelGGL((matrix_os_kernel<KS, WR, 1, true>),
+            hipLaunchKernelGGL((matrix_os_kernel<KS, WR, RPW, true>),
                                dim3(static_cast<unsigned>(blocks)), dim3(O::kThreads), lds, st,
                                a, G, static_cast<int>(C), static_cast<int>(TS));
     } else
@@ -2815,11 +2815,11 @@ inline OsGeom os_geom(int KS, int RB, bool two)
     // region: two row blocks per wave, so one group (k200, k256) or two
     // (k300, k384) stage each input tile instead of two or three (k200
     // decode 0.757 -> 0.66 ms, k300 0.704 -> 0.653, k256 0.30 -> 0.278,
-    // k384 0.88 -> 0.83; encodes ~10 % faster).  Not for the systematic
-    // decodes' two regions (k300 sys decode 1.05 -> 1.41 ms; at KS = 24 that
-    // variant spills), nor at KS = 8 (k128 encode 0.725 -> 0.757 ms;
-    // gpurun_out/ab_r5k, ab_r5l)
-    if ((KS == 16 || KS == 20 || KS == 24) && RB > 8 && !two)
+    // k384 0.88 -> 0.83; encodes ~10 % faster).  The systematic decodes'
+    // two regions too since their rows load once (round 6), but not at KS =
+    // 24 (28 bytes of scratch); not at KS = 8 (k128 encode 0.725 -> 0.757
+    // ms; gpurun_out/ab_r5k, ab_r5l)
+    if ((KS == 16 || KS == 20 || (KS == 24 && !two)) && RB > 8)
         return {8, 2};
     // KS = 40 (384 < k <= 640, K chunks): one row block per wave (80
     // operand VGPRs), one or two source regions
