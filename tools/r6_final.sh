@@ -29,9 +29,14 @@ if [ "$PART" = main ]; then
   done
   timeout -k 10 300 python3 bench.py --cfg cfg3 --systematic --no-cpu-baseline --warmup 60 > $O/bench_cfg3_sys.log 2>&1 || exit $?
   line $O/bench_cfg3_sys.log cfg3_sys
+  for c in k200 k300 k384 k600; do
+    timeout -k 10 300 python3 bench.py --cfg $c --systematic --no-cpu-baseline --warmup 30 > $O/bench_${c}_sys.log 2>&1 || exit $?
+    line $O/bench_${c}_sys.log ${c}_sys
+  done
   for c in cfg2 cfg3 k200 k256 k300 k384 k1000 k600; do
     bash tools/prof.sh $O/prof_$c --cfg $c --steps 10 --warmup $(wu $c) --no-cpu-baseline --no-secondary || exit $?
   done
+  bash tools/prof.sh $O/prof_k600_sys --cfg k600 --systematic --steps 10 --warmup 30 --no-cpu-baseline --no-secondary || exit $?
   timeout -k 10 400 python3 tools/host_rate.py > $O/host_rate.json 2> $O/host_rate.err || exit $?
 else
   bash tools/pmc_roofline.sh $O/pmc_cfg2 cfg2 4096 --no-secondary || exit $?
@@ -39,5 +44,9 @@ else
   for c in "cfg3 1024" "cfg1 100" "k32 1024" "k128 128" "k200 64" "k256 256" "k300 32" "k384 32" "k1000 16" "k600 16" "cfg3p64 64"; do
     set -- $c
     bash tools/pmc_roofline.sh $O/pmc_$1 $1 $2 --cfg $1 --no-secondary || exit $?
+  done
+  for c in "cfg3 1024" "k300 32" "k600 16"; do
+    set -- $c
+    bash tools/pmc_roofline.sh $O/pmc_$1_sys $1_sys $2 --cfg $1 --systematic --no-secondary || exit $?
   done
 fi
