@@ -216,12 +216,14 @@ _craft = craft_oor_columns
 
 
 def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True,
-                     encoder=None, oracle_stripes=None, windows=None):
+                     encoder=None, oracle_stripes=None, windows=None, ids_fn=None):
     """Encode S random stripes, decode each from its own random k-subset,
     through both decode layouts.  check_oracle: the first 3 stripes' outputs
     and OOR lists bit-exact against the oracle; oracle_stripes + windows:
     those stripes' outputs, OOR lists and decodes against the oracle column
-    window by column window (full-size batches)."""
+    window by column window (full-size batches); ids_fn(rng, s): stripe s's
+    received ids, in the order the caller passes them (default: a sorted
+    random k-subset)."""
     torch = _torch()
     import quadiron_amd as qa
     rng = np.random.default_rng(seed)
@@ -256,7 +258,8 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True,
     # set so that a real decode happens)
     ids = np.zeros((S, k), np.uint16)
     for s in range(S):
-        ids[s] = np.sort(rng.choice(k + m, k, replace=False))
+        ids[s] = (ids_fn(rng, s) if ids_fn else
+                  np.sort(rng.choice(k + m, k, replace=False)))
     di = torch.from_numpy(ids.view(np.int16)).cuda()
     # a context buffer full of garbage: the context kernel must write every
     # word the decode reads (it skips the tiles' zero halves at k > 32)
@@ -388,6 +391,38 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True,
 ])
 def test_batch_vs_oracle(k, m, sys_, S, P):
     _batch_roundtrip(k, m, sys_, S, P, seed=k * 1000 + m + P, n_craft=16)
+
+
+@pytest.mark.parametrize("k,m,sys_,S,P", [
+    (16, 48, 1, 6, 2048),     # KS = 1: matrix_mfma_kernel, LDS context
+    (64, 960, 1, 6, 2048),    # matrix_os_kernel<4, ...>, LDS context
+    (200, 56, 1, 6, 1024),    # k > 128 context, KS = 16 at two row blocks per wave
+    (200, 56, 1, 6, 1000),    # the same with dot2 column tails
+    (300, 212, 1, 6, 1024),   # KS = 20
+    (600, 1400, 1, 6, 1024),  # KS = 40, two K chunks
+    (64, 960, 0, 4, 2048),    # non-systematic: any order, nothing reordered
+    (600, 1400, 0, 4, 1024),
+])
+def test_decode_ids_any_order(k, m, sys_, S, P):
+    """Received ids in any order.  The systematic decode contexts list the
+    received fragments region by region (data first: ctx.hip order_ids), and
+    the two-region matrix kernel loads each row once through its region's
+    descriptor, with one extra load for the pass that straddles the
+    boundary; the route entries and the ids the decode reads follow the same
+    order.  Stripes: every data fragment received (shuffled), only parity
+    (m >= k), one data fragment among parity, then shuffled random
+    subsets; OOR columns crafted into the first two stripes' data."""
+    def ids_fn(rng, s):
+        if s == 0:
+            sel = np.arange(k)
+        elif s == 1 and m >= k:
+            sel = k + rng.choice(m, k, replace=False)
+        elif s == 2 and m >= k - 1:
+            sel = np.concatenate([[rng.integers(k)], k + rng.choice(m, k - 1, replace=False)])
+        else:
+            sel = rng.choice(k + m, k, replace=False)
+        return rng.permutation(sel)
+    _batch_roundtrip(k, m, sys_, S, P, seed=31 * k + m + P + sys_, n_craft=16, ids_fn=ids_fn)
 
 
 def _slice_windows(P, W=4096, width=256):
