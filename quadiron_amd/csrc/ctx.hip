@@ -1145,25 +1145,37 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
             atomicOr(err, kErrBadIds);
     }
     if (mode != 0) {
-        // systematic: M[t][i] = Q_i(r^t) / A'(x_i), one thread per row t,
-        // Q_i(r^t) = A(r^t) / (r^t - x_i) (0 when r^t is another received
-        // point, A'(x_i) when it is x_i), the k inverses of a row from one
-        // inversion (prefix products walked back)
+        // systematic: M[t][i] = Q_i(r^t) / A'(x_i), Q_i(r^t) = A(r^t) / (r^t -
+        // x_i) (0 when r^t is another received point, A'(x_i) when it is
+        // x_i).  TPR lanes per row t (2..8: all NT threads busy): each
+        // evaluates a segment of A's k + 1 coefficients at r^t (summed over
+        // the group by shuffles) and inverts a slice of the row's r^t - x_i
+        // at once (prefix products, one inversion, walked back).  (One
+        // thread per row ran the k-step chains serially: cfg3 systematic
+        // context 52 us against 27 us non-systematic.)
         __syncthreads();
-        if (tid < k) {
-            uint32_t* row = Mt + tid * kp;
-            const uint32_t et = canon_lz(rpow_lz(rp, static_cast<uint32_t>(tid), lgn));
-            uint32_t av = 1;  // A(r^t), A monic
-            for (int j = k - 1; j >= 0; j--)
-                av = canon_lz(fold(mul_lz(balanced(av), balanced(et)) + A[j]));
+        const int TPR = NT >= 8 * k ? 8 : NT >= 4 * k ? 4 : NT >= 2 * k ? 2 : 1;
+        const int t = tid / TPR, sub = tid % TPR;
+        if (t < k) {  // uniform in the row's lane group
+            uint32_t* row = Mt + t * kp;
+            const uint32_t et = canon_lz(rpow_lz(rp, static_cast<uint32_t>(t), lgn));
+            const int len = (k + TPR) / TPR;  // ceil((k + 1) / TPR)
+            const int j0 = sub * len, j1 = min(k + 1, j0 + len);
+            uint32_t part = 0;  // sum_{j0 <= j < j1} A[j] (r^t)^(j - j0); A[k] = 1
+            for (int j = j1 - 1; j >= j0; j--)
+                part = canon_lz(fold(mul_lz(balanced(part), balanced(et)) + A[j]));
+            const uint32_t term = j0 < j1 ? mulm(part, powm(et, static_cast<uint32_t>(j0))) : 0u;
+            const uint32_t av = grp_add(term, TPR) % 65537u;  // A(r^t)
+            const int seg = (k + TPR - 1) / TPR;
+            const int i0 = sub * seg, i1 = min(k, i0 + seg);
             uint32_t pre = 1;
-            for (int i = 0; i < k; i++) {
+            for (int i = i0; i < i1; i++) {
                 const uint32_t d = et >= xs[i] ? et - xs[i] : et + 65537u - xs[i];
                 row[i] = pre;
                 pre = canon_lz(mul_lz(balanced(pre), balanced(d ? d : 1u)));
             }
             uint32_t inv = inv_lz(pre);
-            for (int i = k - 1; i >= 0; i--) {
+            for (int i = i1 - 1; i >= i0; i--) {
                 const uint32_t d = et >= xs[i] ? et - xs[i] : et + 65537u - xs[i];
                 const uint32_t inv_i = canon_lz(mul_lz(balanced(inv), balanced(row[i])));
                 inv = canon_lz(mul_lz(balanced(inv), balanced(d ? d : 1u)));
