@@ -95,9 +95,12 @@ size_t qi_gpu_decode_ctx_bytes(const qi_plan* plan, int n_stripes,
                                long long words);
 
 /* Build per-stripe decode contexts from the received fragment ids:
- * d_ids[s*k + i] (u16, ascending, distinct, < k+m) -- the k fragments the
- * decoder uses (FecCode::decode_blocks_vertical picks the first k present,
- * src/fec_base.h:1199-1236) -- and route the OOR marks of those fragments
+ * d_ids[s*k + i] (u16, distinct, < k+m; ascending as the reference passes
+ * them, any order accepted) -- the k fragments the decoder uses
+ * (FecCode::decode_blocks_vertical picks the first k present,
+ * src/fec_base.h:1199-1236; a systematic context lists them data fragments
+ * first, so that the matrix kernel reads each of its two source regions in
+ * one run) -- and route the OOR marks of those fragments
  * (buckets as produced by qi_gpu_encode) into per-tile tables.  With NULL
  * counts the context is built from the ids alone (init_context_dec,
  * src/fec_base.h:758-793: before the fragments' data and marks exist, e.g.
