@@ -342,6 +342,9 @@ def main():
     # 384 < k <= 640 at a whole 1024-word tile: the decode on the matrix
     # cores at KS = 40 in two K chunks (round 6)
     gen_blocks(ref, ora, "blk_k400_m100_w1024", 400, 100, 0, 256, 2048, 55, 1, 10, out)
+    # systematic 384 < k <= 640 (round 6): the encode from the closed-form
+    # Lagrange generator and the two-region decode, both at KS = 40
+    gen_blocks(ref, ora, "blk_k450_m200_sys_w1024", 450, 200, 1, 256, 2048, 56, 1, 10, out)
 
     def gen_scn(*a):
         if not only or a[2] in only:
