@@ -633,7 +633,10 @@ def test_unaligned_rows_whole_tiles(k, m, sys_):
     assert (cnt_h[0] == o_cnt).all() and cnt_h[0].sum() > 0
     for i in range(no):
         assert (np.sort(ent_h[0, i, :cnt_h[0, i]]) == o_oor[i, :o_cnt[i]]).all()
-    ids = np.stack([np.sort(rng.choice(k + m, k, replace=False)) for _ in range(S)])
+    # stripe 1's ids shuffled: the lazily built sections follow the order
+    # the context lists them in (systematic: data fragments first)
+    ids = np.stack([np.sort(rng.choice(k + m, k, replace=False)) if s == 0 else
+                    rng.permutation(rng.choice(k + m, k, replace=False)) for s in range(S)])
     ids = ids.astype(np.uint16)
     di = torch.from_numpy(ids.view(np.int16)).cuda()
     ctx = torch.randint(0, 256, (plan.ctx_bytes(S, P),), dtype=torch.uint8,
