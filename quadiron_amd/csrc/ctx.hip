@@ -270,10 +270,11 @@ constexpr int kTreeBuf = 2 * 512 + 4;
 static_assert(2 * kTreeBuf <= kPackStg, "tree buffers inside the packing stage");
 
 // One pass: NT / LPR rows from row block rb0 on (LPR lanes per row); row
-// t's canonical entries i0 .. i0 + 3 from ent(t, i0, e).  stg: a row per
-// pass row of the (aw, bw) words of each group (LDS).
+// t's canonical entries i0 .. i0 + 3, already column-scaled by 1 / A'(x_i),
+// from ent(t, i0, e).  stg: a row per pass row of the (aw, bw) words of each
+// group (LDS).
 template <int NT, int LPR, class Ent>
-__device__ __forceinline__ void pack_tiles_pass(int rb0, const Ent& ent, const uint32_t* cinv, const MatLayout& L,
+__device__ __forceinline__ void pack_tiles_pass(int rb0, const Ent& ent, const MatLayout& L,
                                 int32_t* mat, uint32_t* stg_base)
 {
     constexpr int ROWS = NT / LPR;
@@ -298,7 +299,7 @@ __device__ __forceinline__ void pack_tiles_pass(int rb0, const Ent& ent, const u
 #pragma unroll
                 for (int jb = 0; jb < 4; jb++) {
                     const int i = i0 + jb;
-                    v[m][jb] = i < k ? mulm(e[jb], cinv[i]) : 0u;
+                    v[m][jb] = i < k ? e[jb] : 0u;
                     bad |= i < k && !coef_ok(balanced(v[m][jb]));
                 }
             }
@@ -763,15 +764,16 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
             // block's chunks [c0, c1) of the stripe's nb blocks, never in
             // global memory: each chunk's rows written into LDS, then its row
             // blocks packed straight into the operand tiles (LPR lanes per
-            // row, 4 entries per lane and group: scale, split, staged, stored
-            // rows-fastest as whole tile lines).  No `plain` rows, no dot2
-            // section (the kernels take single coefficients from the tiles).
+            // row, 4 entries per lane and group: split, staged, stored
+            // rows-fastest as whole tile lines).  The rows are written
+            // column-scaled by 1 / A'(x_i) (off the chains, so the packing
+            // pass does no multiplies).  No `plain` rows, no dot2 section (the
+            // kernels take single coefficients from the tiles).
             //   non-systematic: thread i runs Q_i's synthetic division again
             // (1 / A'(x_i) is known now), from the top down through the rows
             // above the block's chunks without keeping them.
             //   systematic: row t is Q_i(r^t) = A(r^t) / (r^t - x_i), or
-            // A'(x_i) where r^t = x_i (the packing applies the column scale
-            // 1 / A'(x_i)).  TPR lanes per row: each evaluates a segment of A's
+            // A'(x_i) where r^t = x_i (scaled: 1).  TPR lanes per row: each evaluates a segment of A's
             // k + 1 coefficients at r^t (the segments summed across the group
             // by shuffles) and inverts a seg-entry slice of the row's r^t - x_i
             // at once (prefix products, one inversion, walked back).  (One
@@ -792,8 +794,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                 const int lo = CH * c, hi = min(k, lo + CH);
                 if (mode == 0) {
                     if (tid < k) {
+                        const int32_t ci = balanced(cinv[tid]);
                         auto keep = [&](int t, int32_t qt) {
-                            ch[(t - lo) * kpc + tid] = canon_lz(qt);
+                            ch[(t - lo) * kpc + tid] = canon_lz(mul_lz(qt, ci));
                         };
                         if (hi == k)
                             keep(k - 1, q);
@@ -826,7 +829,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                         const uint32_t d = subm(et, xs[i]);
                         const uint32_t inv_i = mulm(inv, row[i]);
                         inv = mulm(inv, d ? d : 1u);
-                        row[i] = d ? mulm(av, inv_i) : aprime[i];
+                        row[i] = d ? mulm(mulm(av, inv_i), cinv[i]) : 1u;
                     }
                 }
                 __syncthreads();
@@ -839,9 +842,9 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
                 };
                 // (ends with a barrier: the chunk buffer is free again)
                 if (CH == kCtxChunk)
-                    pack_tiles_pass<NT, NT / kCtxChunk>(lo >> 4, ent, cinv, L, mat, stg);
+                    pack_tiles_pass<NT, NT / kCtxChunk>(lo >> 4, ent, L, mat, stg);
                 else
-                    pack_tiles_pass<NT, NT / 32>(lo >> 4, ent, cinv, L, mat, stg);
+                    pack_tiles_pass<NT, NT / 32>(lo >> 4, ent, L, mat, stg);
             }
             return;
         }
