@@ -369,6 +369,10 @@ def _batch_roundtrip(k, m, sys_, S, P, seed, n_craft=0, check_oracle=True,
     (385, 127, 1, 2, 1024),
     (600, 1400, 1, 1, 1024),
     (640, 384, 1, 1, 2048),
+    # systematic generators between 2^18 and 2^20 entries (round 6: the
+    # closed-form Lagrange rows made them cheap to build)
+    (300, 1000, 1, 1, 1024),  # KS = 20, 1000 x 300
+    (640, 1600, 1, 1, 1024),  # KS = 40, 1600 x 640 (n = 4096)
     # k > 256: the NTT-structured general path (ntt.hip)
     (257, 255, 0, 1, 300),    # smallest NTT-path code
     (300, 100, 1, 1, 300),    # systematic: interpolation + NTT_n encode
