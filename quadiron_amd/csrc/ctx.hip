@@ -1187,47 +1187,50 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         }
     }
     __syncthreads();
-    // items: (row t, 4-entry group j), rows fastest (16 lanes = 16 rows of
-    // one group: the LDS pitch 4 x odd makes their b128 reads conflict-free)
-    const int KS = L.KS(), KH = 16 * KS, nj = KH / 4, RB = L.RB();
-    const int items = RB * nj * 16;
-    for (int it = tid; it < items; it += NT) {
-        const int tl = it & 15, jj = it >> 4;
-        const int t = 16 * (jj / nj) + tl, i0 = 4 * (jj % nj);
-        if (t >= L.R || i0 >= k)
-            continue;
-        uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
-        const uint4 c4 = *reinterpret_cast<const uint4*>(cinv + i0);
-        uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
-        const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-        for (int jb = 0; jb < 4; jb++)
-            e[jb] = i0 + jb < k ? canon_lz(mul_lz(static_cast<int32_t>(e[jb]), balanced(c[jb])))
-                                : 0u;
-        *reinterpret_cast<uint4*>(Mt + t * kp + i0) = uint4{e[0], e[1], e[2], e[3]};
-    }
-    __syncthreads();
-    // per row: sum, scale test, the rare rescale (4 lanes per row, quad
-    // reductions by DPP; a row needs a unit scale with probability ~5 k /
-    // 65537, i.e. ~27 % of the stripes at k = 64, so the rescale runs on the
-    // quad too: s = 2, 3, ... as pack_row), kcorr / rscale / kmf
+    // one pass per row, 4 lanes per row (quad reductions by DPP), lane sub
+    // holding the 4-entry groups i0 = 4 sub + 16 m in registers: the column
+    // scale 1 / A'(x_i), the row sum and scale test, the rare rescale (a row
+    // needs a unit scale with probability ~5 k / 65537, i.e. ~27 % of the
+    // stripes at k = 64, so it runs on the quad too: s = 2, 3, ... as
+    // pack_row), kcorr / rscale / kmf, and the row's operand tiles.  (Round
+    // 5 ran three passes with a barrier between each: column scale by
+    // items, rows, tiles by items.)
+    const int KS = L.KS(), KH = 16 * KS, RB = L.RB();
+    int32_t* mf = mat + L.mf();
     {
+        constexpr int MG = 8;  // k <= 128: at most 8 groups per lane
         const int sub = tid & 3;
-        for (int t0 = 0; t0 < L.R; t0 += NT / 4) {
+        for (int t0 = 0; t0 < 16 * RB || t0 < L.R; t0 += NT / 4) {
             const int t = t0 + tid / 4;
+            uint32_t* row = Mt + t * kp;
             uint32_t sum = 0, bad = 0;
-            if (t < L.R) {
-                for (int i0 = 4 * sub; i0 < k; i0 += 16) {
-                    const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
-                    sum += e4.x + e4.y + e4.z + e4.w;  // padding entries are 0
-                    bad |= coef_bad(e4.x) | coef_bad(e4.y) | coef_bad(e4.z) | coef_bad(e4.w);
+            uint4 ev[MG];
+#pragma unroll
+            for (int m = 0; m < MG; m++) {
+                const int i0 = 4 * sub + 16 * m;
+                ev[m] = uint4{0u, 0u, 0u, 0u};
+                if (t < L.R && i0 < k) {
+                    const uint4 e4 = *reinterpret_cast<const uint4*>(row + i0);
+                    const uint4 c4 = *reinterpret_cast<const uint4*>(cinv + i0);
+                    uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
+                    const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+                    for (int jb = 0; jb < 4; jb++) {
+                        e[jb] = i0 + jb < k ? canon_lz(mul_lz(static_cast<int32_t>(e[jb]),
+                                                              balanced(c[jb])))
+                                            : 0u;
+                        sum += e[jb];
+                        bad |= coef_bad(e[jb]);
+                    }
+                    ev[m] = uint4{e[0], e[1], e[2], e[3]};
+                    *reinterpret_cast<uint4*>(row + i0) = ev[m];
                 }
             }
             bad |= __builtin_amdgcn_update_dpp(0u, bad, 0xB1, 0xf, 0xf, false);
             bad |= __builtin_amdgcn_update_dpp(0u, bad, 0x4E, 0xf, 0xf, false);
             int32_t rs = 1;
-            if (bad) {  // quad-uniform, rare
-                uint32_t* row = Mt + t * kp;
+            if (bad) {  // quad-uniform, rare; the quad's scaled entries are in
+                        // LDS (one wave: its LDS accesses complete in order)
                 uint32_t sc = 0;
                 for (uint32_t cand = 2; cand < 256 && !sc; cand++) {
                     // |s^-1| <= 32766 (the epilogue's v_mul_i32_i24)
@@ -1251,57 +1254,63 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
                     row[i] = canon_lz(static_cast<int32_t>(row[i] * (sc ? sc : 1u)));
                     sum += row[i];
                 }
+                // the lane's groups back from the rescaled row
+#pragma unroll
+                for (int m = 0; m < MG; m++) {
+                    const int i0 = 4 * sub + 16 * m;
+                    if (i0 < k)
+                        ev[m] = *reinterpret_cast<const uint4*>(row + i0);
+                }
             }
             sum += __builtin_amdgcn_update_dpp(0u, sum, 0xB1, 0xf, 0xf, false);
             sum += __builtin_amdgcn_update_dpp(0u, sum, 0x4E, 0xf, 0xf, false);
-            if (t >= L.R || sub != 0)
-                continue;
-            // sum < 2^24: two folds, then canonical
-            const uint32_t sq = canon_lz(fold(static_cast<int32_t>(sum)));
-            mat[L.kcorr() + t] = static_cast<int32_t>(canon_lz(mul_lz(balanced(sq), 32768)));
-            mat[L.rscale() + t] = rs;
-            if (KS) {
-                mat[L.kmf() + t] = static_cast<int32_t>(canon_lz(mul_lz(balanced(sq), 32896)));
-                mat[L.rscale_mf() + t] = rs;
+            if (t < L.R && sub == 0) {
+                // sum < 2^24: two folds, then canonical
+                const uint32_t sq = canon_lz(fold(static_cast<int32_t>(sum)));
+                mat[L.kcorr() + t] = static_cast<int32_t>(canon_lz(mul_lz(balanced(sq), 32768)));
+                mat[L.rscale() + t] = rs;
+                if (KS) {
+                    mat[L.kmf() + t] = static_cast<int32_t>(canon_lz(mul_lz(balanced(sq), 32896)));
+                    mat[L.rscale_mf() + t] = rs;
+                }
             }
-        }
-    }
-    __syncthreads();
-    // the operand tiles (pack_mf_dword's layout: [a | 0], [0 | b], [b | a];
-    // the zero halves are not written at KS >= 4, the kernel never reads
-    // them): items rows-fastest, so a wave's stores fill whole tile lines
-    int32_t* mf = mat + L.mf();
-    if (KS) {
-        for (int it = tid; it < items; it += NT) {
-            const int tl = it & 15, jj = it >> 4;
-            const int j = jj % nj, rb = jj / nj;
-            const int t = 16 * rb + tl, i0 = 4 * j;
-            uint32_t aw = 0, bw = 0;
-            if (t < L.R && i0 < k) {
-                const uint4 e4 = *reinterpret_cast<const uint4*>(Mt + t * kp + i0);
-                const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
+            // the operand tiles (pack_mf_dword's layout: [a | 0], [0 | b],
+            // [b | a]; the zero halves are not written at KS >= 4, the kernel
+            // never reads them), zeros past the rows and entries: a wave
+            // holds 16 rows of one row block, so each store fills 64
+            // consecutive dwords of a tile
+            if (!KS || t >= 16 * RB)
+                continue;
+            const int rb = t >> 4, tl = t & 15;
+#pragma unroll
+            for (int m = 0; m < MG; m++) {
+                const int i0 = 4 * sub + 16 * m;
+                if (m >= KS)  // groups j = sub + 4 m < KH / 4
+                    break;
+                const uint32_t e[4] = {ev[m].x, ev[m].y, ev[m].z, ev[m].w};
+                uint32_t aw = 0, bw = 0;
 #pragma unroll
                 for (int jb = 0; jb < 4; jb++) {
-                    if (i0 + jb < k) {
+                    if (i0 + jb < k) {  // (entries past k and rows past R are 0)
                         int32_t a, b;
                         split_i8(e[jb], a, b);
                         aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
                         bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
                     }
                 }
-            }
 #pragma unroll
-            for (int half = 0; half < 2; half++) {
-                const int K = half * KH + i0;
-                const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
-                const size_t base =
-                    static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl) * 2 + dw;
-                if (KS < 4 || half == 0)
-                    mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
-                if (KS < 4 || half == 1)
-                    mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
-                if (KS < 2)  // [b | a]: the kernels rebuild it at KS >= 2
-                    mf[base + 256] = static_cast<int32_t>(half ? aw : bw);
+                for (int half = 0; half < 2; half++) {
+                    const int K = half * KH + i0;
+                    const int ks = K >> 5, g = (K & 31) >> 3, dw = (K & 7) >> 2;
+                    const size_t base =
+                        static_cast<size_t>((rb * KS + ks) * 3) * 128 + (16 * g + tl) * 2 + dw;
+                    if (KS < 4 || half == 0)
+                        mf[base] = static_cast<int32_t>(half ? 0u : aw);        // [a | 0]
+                    if (KS < 4 || half == 1)
+                        mf[base + 128] = static_cast<int32_t>(half ? bw : 0u);  // [0 | b]
+                    if (KS < 2)  // [b | a]: the kernels rebuild it at KS >= 2
+                        mf[base + 256] = static_cast<int32_t>(half ? aw : bw);
+                }
             }
         }
     }
@@ -1315,6 +1324,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
     // scattered over the rows had made the round-1 context store-bound)
     if (!dot2)
         return;
+    __syncthreads();  // every row final (the pass above is row-local)
     int32_t* plain = mat + L.plain();
     const int ng = (k + 3) / 4;
     for (int it = tid; it < L.R * ng; it += NT) {
