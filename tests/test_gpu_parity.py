@@ -400,25 +400,27 @@ def test_batch_vs_oracle(k, m, sys_, S, P):
 def _random_shapes(n, seed):
     """n codes drawn from a fixed seed: k near every routing boundary (the
     matrix-core K-steps, the context kernels, the NTT engine) or uniform up
-    to 700, m small (erasure decode), medium or large, n <= 4096, ragged and
-    whole-tile widths, both code types."""
+    to 700, m small (erasure decode), medium, large or very large (n up to
+    16384: the multi-pass engine), ragged and whole-tile widths, both code
+    types."""
     rng = np.random.default_rng(seed)
     edges = [1, 2, 3, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129, 255, 256,
              257, 319, 320, 321, 383, 384, 385, 639, 640, 641, 1000]
     shapes = []
     while len(shapes) < n:
         k = int(rng.choice(edges)) if rng.random() < 0.6 else int(rng.integers(1, 700))
-        kind = int(rng.integers(3))
+        kind = int(rng.integers(4))
         m = (int(rng.integers(1, 65)) if kind == 0 else
-             int(rng.integers(1, 400)) if kind == 1 else int(rng.integers(400, 3000)))
-        if k + m > 4096:
+             int(rng.integers(1, 400)) if kind == 1 else
+             int(rng.integers(400, 3000)) if kind == 2 else int(rng.integers(3000, 12000)))
+        if k + m > 16384:
             continue
         P = int(rng.choice([int(rng.integers(1, 64)), int(rng.integers(64, 1200)), 1024, 2048]))
         shapes.append((k, m, int(rng.integers(2)), int(rng.integers(1, 4)), P))
     return shapes
 
 
-@pytest.mark.parametrize("k,m,sys_,S,P", _random_shapes(32, 20261019))
+@pytest.mark.parametrize("k,m,sys_,S,P", _random_shapes(64, 20261019))
 def test_random_shapes_vs_oracle(k, m, sys_, S, P):
     """A seeded sweep beyond the hand-picked shapes above: encode outputs and
     OOR lists of the first stripes bit-exact against the oracle, every
