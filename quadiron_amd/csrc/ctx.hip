@@ -977,7 +977,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
 {
     __shared__ uint32_t xs[128];
     __shared__ int32_t A[129];        // balanced coefficients of A(x)
-    __shared__ __attribute__((aligned(16))) uint32_t cinv[128];  // 1 / A'(x_i)
+    __shared__ __attribute__((aligned(16))) int32_t cinv[128];  // 1 / A'(x_i), balanced
     __shared__ uint32_t aprime[128];  // A'(x_i)
     __shared__ uint16_t pid[128];     // the ids in the context's order
     __shared__ int wtot[NT / 64];
@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
         }
         const uint32_t ap = canon_lz(fold(h));
         aprime[tid] = ap;
-        cinv[tid] = inv_lz(ap);
+        cinv[tid] = balanced(inv_lz(ap));
         if (ap == 0u)  // repeated ids
             atomicOr(err, kErrBadIds);
     }
@@ -1211,23 +1211,33 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
                 ev[m] = uint4{0u, 0u, 0u, 0u};
                 if (t < L.R && i0 < k) {
                     const uint4 e4 = *reinterpret_cast<const uint4*>(row + i0);
-                    const uint4 c4 = *reinterpret_cast<const uint4*>(cinv + i0);
+                    const int4 c4 = *reinterpret_cast<const int4*>(cinv + i0);
                     uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
-                    const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+                    const int32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
 #pragma unroll
                     for (int jb = 0; jb < 4; jb++) {
-                        e[jb] = i0 + jb < k ? canon_lz(mul_lz(static_cast<int32_t>(e[jb]),
-                                                              balanced(c[jb])))
-                                            : 0u;
+                        // canonical by one min3: fold(y) is in [-q, 2q)
+                        const int32_t f = fold(mul_lz(static_cast<int32_t>(e[jb]), c[jb]));
+                        const uint32_t fu = static_cast<uint32_t>(f);
+                        e[jb] = i0 + jb < k ? min(min(fu, fu + 65537u), fu - 65537u) : 0u;
                         sum += e[jb];
                         bad |= coef_bad(e[jb]);
                     }
                     ev[m] = uint4{e[0], e[1], e[2], e[3]};
-                    *reinterpret_cast<uint4*>(row + i0) = ev[m];
                 }
             }
             bad |= __builtin_amdgcn_update_dpp(0u, bad, 0xB1, 0xf, 0xf, false);
             bad |= __builtin_amdgcn_update_dpp(0u, bad, 0x4E, 0xf, 0xf, false);
+            // the scaled row back to LDS only where it is read again: the
+            // rare rescale below (quad-uniform) and the dot2 sections
+            if (bad || dot2) {
+#pragma unroll
+                for (int m = 0; m < MG; m++) {
+                    const int i0 = 4 * sub + 16 * m;
+                    if (t < L.R && i0 < k)
+                        *reinterpret_cast<uint4*>(row + i0) = ev[m];
+                }
+            }
             int32_t rs = 1;
             if (bad) {  // quad-uniform, rare; the quad's scaled entries are in
                         // LDS (one wave: its LDS accesses complete in order)
@@ -1287,17 +1297,26 @@ __global__ __launch_bounds__(NT) void decode_ctx_lds_kernel(
                 const int i0 = 4 * sub + 16 * m;
                 if (m >= KS)  // groups j = sub + 4 m < KH / 4
                     break;
+                // split_i8 of the 4 entries (0 past k and past R: a = b = 0):
+                // v = 256 a + b in [-32896, 32639], b = the signed low byte
+                // of v, a = (v - b) / 256; entry jb's bytes into byte jb of
+                // aw / bw by three byte permutes each
                 const uint32_t e[4] = {ev[m].x, ev[m].y, ev[m].z, ev[m].w};
-                uint32_t aw = 0, bw = 0;
+                uint32_t vb[4], va[4];
 #pragma unroll
                 for (int jb = 0; jb < 4; jb++) {
-                    if (i0 + jb < k) {  // (entries past k and rows past R are 0)
-                        int32_t a, b;
-                        split_i8(e[jb], a, b);
-                        aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
-                        bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
-                    }
+                    int32_t v = balanced(e[jb]);
+                    v = v > 32639 ? v - kQ : v;
+                    const int32_t b = (v << 24) >> 24;
+                    vb[jb] = static_cast<uint32_t>(v);      // b's byte: byte 0
+                    va[jb] = static_cast<uint32_t>(v - b);  // a's byte: byte 1
                 }
+                const uint32_t bw = __builtin_amdgcn_perm(
+                    __builtin_amdgcn_perm(vb[3], vb[2], 0x0c0c0400u),
+                    __builtin_amdgcn_perm(vb[1], vb[0], 0x0c0c0400u), 0x05040100u);
+                const uint32_t aw = __builtin_amdgcn_perm(
+                    __builtin_amdgcn_perm(va[3], va[2], 0x0c0c0501u),
+                    __builtin_amdgcn_perm(va[1], va[0], 0x0c0c0501u), 0x05040100u);
 #pragma unroll
                 for (int half = 0; half < 2; half++) {
                     const int K = half * KH + i0;

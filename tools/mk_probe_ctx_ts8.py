@@ -25,10 +25,10 @@ rep("""    int32_t* mat = ctx + s * ctx_stride;
     QI_TS(0);
     const int kp = ctx_pitch(k);
     uint32_t* Mt = qi_ctx_lds;""")
-rep("""    order_ids_v<NT>(id_ld, k, mode != 0 && !by_pos, pid, wtot);
-    auto rpow_tab""", """    order_ids_v<NT>(id_ld, k, mode != 0 && !by_pos, pid, wtot);
-    QI_TS(1);
-    auto rpow_tab""")
+rep("""    // x_i = r^{id_i}: thread tid takes point tid (its Q chain below); wave 0
+    // also point 64 + lane""", """    QI_TS(1);
+    // x_i = r^{id_i}: thread tid takes point tid (its Q chain below); wave 0
+    // also point 64 + lane""")
 rep("""    int32_t ab0 = 0;  // wave 0: balanced A[lane] (k <= 64), for the Q chains
     if (tid < 64) {""", """    int32_t ab0 = 0;  // wave 0: balanced A[lane] (k <= 64), for the Q chains
     QI_TS(2);
