@@ -257,6 +257,35 @@ __device__ __forceinline__ void pack_row_grp(uint32_t* row, const uint32_t* csca
 // 120 -> 114 us, k300 179 -> 161 us, k384 219 -> 206 us); 32 rows above
 // k = 384 (a 64 x 640 chunk would not fit LDS)
 constexpr int kCtxChunk = 64;
+
+// a canonical entry a row may not hold unscaled (!coef_ok): the dot2
+// kernel needs |balanced| <= 32766, the i8 split anything but 32640
+__device__ __forceinline__ bool coef_bad(uint32_t e)
+{
+    return e - 32767u < 4u || e == 32640u;
+}
+
+// split_i8 of 4 canonical entries, entry jb's bytes into byte jb of aw / bw:
+// v = 256 a + b in [-32896, 32639], b = the signed low byte of v (b's byte =
+// v's low byte), a = (v - b) / 256 (a's byte = byte 1 of v - b); three byte
+// permutes per word
+__device__ __forceinline__ void split_i8_x4(const uint32_t (&e)[4], uint32_t& aw, uint32_t& bw)
+{
+    uint32_t vb[4], va[4];
+#pragma unroll
+    for (int jb = 0; jb < 4; jb++) {
+        int32_t v = balanced(e[jb]);
+        v = v > 32639 ? v - kQ : v;
+        const int32_t b = (v << 24) >> 24;
+        vb[jb] = static_cast<uint32_t>(v);
+        va[jb] = static_cast<uint32_t>(v - b);
+    }
+    bw = __builtin_amdgcn_perm(__builtin_amdgcn_perm(vb[3], vb[2], 0x0c0c0400u),
+                               __builtin_amdgcn_perm(vb[1], vb[0], 0x0c0c0400u), 0x05040100u);
+    aw = __builtin_amdgcn_perm(__builtin_amdgcn_perm(va[3], va[2], 0x0c0c0501u),
+                               __builtin_amdgcn_perm(va[1], va[0], 0x0c0c0501u), 0x05040100u);
+}
+
 __host__ __device__ inline int ctx_chunk(int k)
 {
     return k > kMatGenMaxKin ? 32 : kCtxChunk;
@@ -300,7 +329,7 @@ __device__ __forceinline__ void pack_tiles_pass(int rb0, const Ent& ent, const M
                 for (int jb = 0; jb < 4; jb++) {
                     const int i = i0 + jb;
                     v[m][jb] = i < k ? e[jb] : 0u;
-                    bad |= i < k && !coef_ok(balanced(v[m][jb]));
+                    bad |= coef_bad(v[m][jb]);  // (0 past k: never bad)
                 }
             }
             bad = grp_or(bad, LPR);
@@ -323,21 +352,19 @@ __device__ __forceinline__ void pack_tiles_pass(int rb0, const Ent& ent, const M
             uint32_t sum = 0;
 #pragma unroll
             for (int m = 0; m < MM; m++) {
-                uint32_t aw = 0, bw = 0;
+                const int jg = sub + m * LPR;
+                if (jg >= nj)
+                    break;
+                // (entries past k are 0: a = b = 0, nothing added)
+                uint32_t c[4];
 #pragma unroll
                 for (int jb = 0; jb < 4; jb++) {
-                    const int i = 4 * (sub + m * LPR) + jb;
-                    if (i < k) {
-                        const uint32_t c = sc == 1 ? v[m][jb] : mulm(v[m][jb], sc);
-                        sum += c;
-                        int32_t a, b;
-                        split_i8(c, a, b);
-                        aw |= (static_cast<uint32_t>(a) & 0xffu) << (8 * jb);
-                        bw |= (static_cast<uint32_t>(b) & 0xffu) << (8 * jb);
-                    }
+                    c[jb] = sc == 1 ? v[m][jb] : mulm(v[m][jb], sc);
+                    sum += c[jb];
                 }
-                const int jg = sub + m * LPR;
-                if (jg < nj) {
+                uint32_t aw, bw;
+                split_i8_x4(c, aw, bw);
+                {
                     stg(rl, 2 * jg) = aw;
                     stg(rl, 2 * jg + 1) = bw;
                 }
@@ -949,13 +976,6 @@ __global__ __launch_bounds__(NT) void decode_ctx_kernel(
 // (shuffle reductions per row group) and 14 in the A(x) / Q chains
 // (ds_bpermute shifts, canonical mulm at every step).
 // ---------------------------------------------------------------------------
-// entries a row may hold (coef_ok on a canonical residue): the dot2 kernel
-// needs |balanced| <= 32766, the i8 split anything but 32640
-__device__ __forceinline__ bool coef_bad(uint32_t e)
-{
-    return e - 32767u < 4u || e == 32640u;
-}
-
 // r^(2^b), balanced, b < 16: x = r^id by at most log2(n) multiplies
 struct RPow2 {
     int32_t v[16];
