@@ -741,29 +741,48 @@ __device__ __forceinline__ void stage_route_marks(const uint32_t* rm, int n_rm,
     }
 }
 
-// The same from the route-table entry rt (count + kRouteCap entries) read
-// by scalar loads (constant address space): a vector load here is ordered
-// with the kernel's streaming stores and its row prefetch in vmcnt, so
-// waiting for it drained both every tile.  Returns the count, or -1 when the
-// tile overflowed the table (scan the buckets).
+// The same from the route-table entry rt (count + kRouteCap entries), the
+// count by a scalar load (constant address space).  VEC: the entries by the
+// lanes that stage one, with a vector load; otherwise all 16 dwords by
+// scalar loads (round 5: a vector load is ordered with the kernel's
+// streaming stores and row prefetch in vmcnt, and waiting for it drained
+// both every tile).  The callers stage a route tile's list once per mark
+// buffer, and only wave 0 issues the vector load; the 16 SGPRs of the
+// scalar form had pushed the KS = 4 kernel to ~75 SGPR spills (VEC there:
+// cfg3 decode -2 us, k200 / k300 -1 %; at KS = 8 the scalar form measured
+// 1.5 % faster, k128).  Returns the count, or -1 when the tile overflowed
+// the table (scan the buckets).
+template <bool VEC>
 __device__ __forceinline__ int stage_route_marks_s(const uint32_t* rt, long long col0, int* s_i,
                                                    uint32_t* s_col)
 {
     using CU = const __attribute__((address_space(4))) uint32_t;
     CU* c = (CU*)rt;
-    uint32_t e[kRouteStride];
+    if constexpr (!VEC) {
+        uint32_t e[kRouteStride];
 #pragma unroll
-    for (int i = 0; i < kRouteStride; i++)
-        e[i] = c[i];
-    const uint32_t rc = e[0];
+        for (int i = 0; i < kRouteStride; i++)
+            e[i] = c[i];
+        const uint32_t rc = e[0];
+        if (rc > static_cast<uint32_t>(kRouteCap))
+            return -1;
+        const int tid = static_cast<int>(threadIdx.x);
+        if (tid < static_cast<int>(rc)) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int i = 0; i < kRouteCap; i++)
+                v = tid == i ? e[1 + i] : v;
+            s_i[tid] = static_cast<int>(v >> 16);
+            s_col[tid] = static_cast<uint32_t>(col0 / kRouteTile * kRouteTile + (v & 0xffffu));
+        }
+        return static_cast<int>(rc);
+    }
+    const uint32_t rc = c[0];
     if (rc > static_cast<uint32_t>(kRouteCap))
         return -1;
     const int tid = static_cast<int>(threadIdx.x);
     if (tid < static_cast<int>(rc)) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int i = 0; i < kRouteCap; i++)
-            v = tid == i ? e[1 + i] : v;
+        const uint32_t v = rt[1 + tid];
         s_i[tid] = static_cast<int>(v >> 16);
         s_col[tid] = static_cast<uint32_t>(col0 / kRouteTile * kRouteTile + (v & 0xffffu));
     }
@@ -2125,16 +2144,45 @@ __global__ __launch_bounds__(512) void matrix_os_kernel(MatArgs a, int G, int C,
         return reinterpret_cast<int*>(qi_lds + O::kMarkOff + 2 * 2 * 4 * kMaxTileOor) + mb;
     };
     const bool marks_in = in_oor.counts != nullptr;
+    // the route-table list each mark buffer holds (block-uniform): the tiles
+    // of one kRouteTile-column route tile share its list (the epilogue keeps
+    // the marks in its own columns), so a buffer that already holds it is not
+    // staged again.  (Staging it every tile cost the cfg3 decode ~8 us: the
+    // wait for the scalar load also drained the LDS accesses in flight,
+    // tools/ab/probe_os_nomarks.patch)
+    // (not at KS = 8, whose kernel measured faster staging every tile from
+    // scalar loads: k128 decode 1.5 %)
+    constexpr bool kOnce = KS != 8;
+    int srt0 = -1, srt1 = -1, scnt0 = 0, scnt1 = 0;
     auto stage_marks = [&](int tile, int mb) -> int {
         if (!marks_in)
             return 0;
         const long long col0 = static_cast<long long>(tile) * NCOL;
         if (a.route) {
-            const int rc = stage_route_marks_s(
-                a.route + s * a.rstride + (col0 / kRouteTile) * kRouteStride, col0, s_i(mb),
-                s_col(mb));
-            if (rc >= 0)
+            const int rti = static_cast<int>(col0 / kRouteTile);
+            if (kOnce && (mb ? srt1 : srt0) == rti)
+                return mb ? scnt1 : scnt0;
+            const int rc = stage_route_marks_s<kOnce>(
+                a.route + s * a.rstride + static_cast<long long>(rti) * kRouteStride, col0,
+                s_i(mb), s_col(mb));
+            if (rc >= 0) {
+                if constexpr (kOnce) {
+                    if (mb) {
+                        srt1 = rti;
+                        scnt1 = rc;
+                    } else {
+                        srt0 = rti;
+                        scnt0 = rc;
+                    }
+                }
                 return rc;
+            }
+        }
+        if constexpr (kOnce) {
+            if (mb)  // this buffer now holds a bucket scan of one tile
+                srt1 = -1;
+            else
+                srt0 = -1;
         }
         OorScan sc{in_oor, sid, src.by_pos, a.slot_base, kin, s, false};
         const int cnt = scan_tile_marks(sc, col0, col0 + NCOL, a.words, s_cnt(mb), s_i(mb),
